@@ -1,0 +1,122 @@
+/*
+ * sparc_amp.h — C ABI of the MI355X (gfx950) SPARC AMP decoder.
+ *
+ * Library: sparc_ldpc_amd/libsparc_amp.so (hipcc --offload-arch=gfx950).
+ *
+ * The reference (Spimp/sparc_ldpc) has no native boundary on this path: the
+ * whole AMP decoder is Python/NumPy.  These entry points replace the Python
+ * functions named on each declaration, with the reference's own native
+ * boundary conventions (ldpc/py/ldpc.py:859-929 -> ldpc/src/c_ldpc.c:32-113):
+ * plain pointers and sizes, caller-allocated outputs, int status returns,
+ * no Python objects across the ABI.  fp64 at the ABI (the reference computes
+ * in fp64); fp32 or fp64 on the device (precision argument of sa_create).
+ *
+ * Status codes: 0 = OK, < 0 = error (sa_last_error() describes the last one
+ * raised on the calling thread).  A context is bound to one device and one
+ * HIP stream; it is not thread-safe, but contexts on different devices may be
+ * driven concurrently from different threads.
+ */
+#ifndef SPARC_AMP_H
+#define SPARC_AMP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct sa_ctx sa_ctx;
+
+enum {
+  SA_OK = 0,
+  SA_ERR_ARG = -1,          /* bad size / shape / pointer (reference: AssertionError) */
+  SA_ERR_HIP = -2,          /* HIP runtime failure */
+  SA_ERR_NOMEM = -3,        /* device allocation failed (reference: c_ldpc.c:40-42 -> -1) */
+  SA_ERR_ORDERING = -4,     /* ordering row not distinct / out of [1, w) */
+  SA_ERR_UNSUPPORTED = -5,  /* configuration outside this backend's limits */
+  SA_ERR_NO_DEVICE = -6     /* no HIP device visible */
+};
+
+enum {
+  SA_BACKEND_HADAMARD = 0,  /* matrix-free sub-sampled Walsh-Hadamard operator (default) */
+  SA_BACKEND_DENSE = 1      /* materialised n x (L*M) fp32 design matrix, GEMV-streamed */
+};
+
+enum { SA_PREC_F32 = 0, SA_PREC_F64 = 1 };
+
+/* sa_amp / sa_run flags */
+enum {
+  SA_FLAG_NO_EARLY_STOP = 1, /* run exactly T iterations (ignore the tau == last_tau stop) */
+  SA_FLAG_BETA0 = 0x100      /* sa_run: start from the beta0 staged by sa_stage */
+};
+
+/* Replaces sparc_transforms(L, M, n, seed) / block_sub_fht(n, M, L, ordering)
+ * (ldpc/sparc_ldpc.py:140-147, :81-136): builds the design operator of L
+ * sections of M columns over n rows from `ordering` (L x n, row-major,
+ * values in [1, w), w = 2^ceil(log2(max(M+1, n+1))), distinct per row) on
+ * `device`.  The ordering itself is generated on the host by the caller with
+ * the reference's RandomState algorithm (sparc_ldpc.py:107-117). */
+int sa_create(sa_ctx** out, int L, int M, int n, const uint32_t* ordering,
+              int backend, int precision, int device);
+
+/* Replaces sparc_transforms_shorter(L, M, n, ordering[sections])
+ * (ldpc/sparc_ldpc.py:154-168; called with a fancy-indexed subset at
+ * ldpc/amp_exit.py:113-116): a new context over the given parent sections. */
+int sa_subset(const sa_ctx* parent, const int64_t* sections, int Ls, sa_ctx** out);
+
+void sa_destroy(sa_ctx* ctx);
+
+/* Replaces the Ab closure, sparc_ldpc.py:143-144 (-> block_sub_fht.Ax
+ * :120-126): out[b] = A beta[b] for B codewords.  beta: B x (L*M), out: B x n. */
+int sa_Ab(sa_ctx* ctx, int B, const double* beta, double* out);
+
+/* Replaces the Az closure, sparc_ldpc.py:145-146 (-> block_sub_fht.Ay
+ * :128-134): out[b] = A^T z[b].  z: B x n, out: B x (L*M). */
+int sa_Az(sa_ctx* ctx, int B, const double* z, double* out);
+
+/* Replaces amp(y, sigma_n, Pl, L, M, T, Ab, Az, beta) (sparc_ldpc.py:189-222)
+ * and amp_test (ldpc/amp_test.py:14-50) for B independent codewords sharing
+ * the operator: y: B x n; Pl: L section powers; beta0: B x (L*M) or NULL for
+ * the zero start; beta_out: B x (L*M); iters_out (may be NULL): per codeword
+ * the loop index at which the exact tau == last_tau stop fired, or T when
+ * the loop ran to completion.  sigma_n is not an argument: the reference
+ * never reads it. */
+int sa_amp(sa_ctx* ctx, int B, const double* y, const double* Pl, int T,
+           const double* beta0, double* beta_out, int* iters_out, int flags);
+
+/* ---- device-resident path (bench / Monte-Carlo harness) ----------------
+ * sa_reserve sizes the device workspace for B codewords and T iterations
+ * (it discards staged data when it has to grow); sa_stage copies y (and Pl, and optionally beta0) into the context's device
+ * buffers; sa_run decodes the staged batch asynchronously on the context's
+ * stream (replayed hipGraph); sa_wait blocks until it is done; sa_fetch
+ * copies the results back.  sa_run_event_ms returns the device time of the
+ * last sa_run measured with HIP events on the context's stream. */
+int sa_reserve(sa_ctx* ctx, int B, int T);
+int sa_stage(sa_ctx* ctx, int B, const double* y, const double* Pl, const double* beta0);
+int sa_run(sa_ctx* ctx, int B, int T, int flags);
+int sa_wait(sa_ctx* ctx);
+int sa_fetch(sa_ctx* ctx, int B, double* beta_out, int* iters_out);
+double sa_run_event_ms(sa_ctx* ctx);
+
+/* Per-kernel device time of one EAGER decode of the staged batch (every
+ * launch bracketed by HIP events on the context's stream).  out[11]:
+ * {mean ms, launches} for kernel kinds 0 section (k_sec), 1 row (k_row),
+ * 2 dense A^T z GEMV, 3 dense denoiser, 4 dense A beta GEMV; out[10] = total
+ * ms of the sequence.  Leaves the decode's results in place like sa_run. */
+int sa_profile(sa_ctx* ctx, int B, int T, int flags, double* out);
+
+/* Per-codeword section decisions (sparc_ldpc.py:452-455: argmax per
+ * section, first index on ties) of the last sa_run / sa_amp, computed on
+ * device: idx_out is B x L. */
+int sa_decide(sa_ctx* ctx, int B, int32_t* idx_out);
+
+/* Introspection. */
+int sa_info(const sa_ctx* ctx, int64_t* out8); /* L, M, n, w, backend, precision, device, bytes */
+int sa_device_count(void);
+const char* sa_last_error(void);
+const char* sa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPARC_AMP_H */

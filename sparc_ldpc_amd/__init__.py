@@ -1,0 +1,16 @@
+"""sparc_ldpc_amd — MI355X (gfx950) SPARC AMP decoder.
+
+Drop-in for the AMP hot path of Spimp/sparc_ldpc (ldpc/sparc_ldpc.py:14-222,
+ldpc/amp_test.py:14-50): the same names, argument order and return shapes,
+with the design operator and the whole iteration loop running as HIP kernels
+in ``libsparc_amp.so`` (C ABI: include/sparc_amp.h).  There is no CPU
+fallback: without the library or a HIP device every call raises.
+"""
+from ._lib import SparcAmpError, load as load_library
+from .operators import (SparcOperator, AbOp, AzOp, make_ordering, sub_fht, block_sub_fht,
+                        sparc_transforms, sparc_transforms_shorter, default_device)
+from .amp import amp, amp_test, amp_batch, operator_of
+from .harness import (SPARCParams, LDPCParams, pa_parameterised, bits2indices, ber_of,
+                      amp_ldpc_sim, mc_decode, ebno_to_sigma, waterfall_plain, amp_test_reps)
+
+__version__ = "0.1.0"

@@ -1,0 +1,107 @@
+"""ctypes binding of the gfx950 HIP library ``libsparc_amp.so`` (include/sparc_amp.h).
+
+The loader follows the reference's own native-boundary pattern
+(ldpc/py/ldpc.py:859-872: ``ctypes.CDLL`` + ``ndarray.ctypes`` pointers,
+caller-allocated outputs, int status codes) but resolves the library next to
+this file instead of relative to the CWD.  There is no CPU fallback: if the
+library is missing or no HIP device is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+import numpy as np
+
+LIB_NAME = "libsparc_amp.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+SA_OK = 0
+SA_ERR_ARG = -1
+SA_ERR_HIP = -2
+SA_ERR_NOMEM = -3
+SA_ERR_ORDERING = -4
+SA_ERR_UNSUPPORTED = -5
+SA_ERR_NO_DEVICE = -6
+
+SA_BACKEND_HADAMARD = 0
+SA_BACKEND_DENSE = 1
+SA_PREC_F32 = 0
+SA_PREC_F64 = 1
+SA_FLAG_NO_EARLY_STOP = 1
+SA_FLAG_BETA0 = 0x100
+
+# Every symbol include/sparc_amp.h declares (tests check the export table).
+EXPORTS = (
+    "sa_create", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
+    "sa_reserve", "sa_stage", "sa_run", "sa_wait", "sa_fetch", "sa_run_event_ms",
+    "sa_profile", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
+)
+
+_P = ct.c_void_p
+_I = ct.c_int
+_D = ct.POINTER(ct.c_double)
+_SIG = {
+    "sa_create": (_I, [ct.POINTER(_P), _I, _I, _I, ct.POINTER(ct.c_uint32), _I, _I, _I]),
+    "sa_subset": (_I, [_P, ct.POINTER(ct.c_int64), _I, ct.POINTER(_P)]),
+    "sa_destroy": (None, [_P]),
+    "sa_Ab": (_I, [_P, _I, _D, _D]),
+    "sa_Az": (_I, [_P, _I, _D, _D]),
+    "sa_amp": (_I, [_P, _I, _D, _D, _I, _D, _D, ct.POINTER(ct.c_int), _I]),
+    "sa_reserve": (_I, [_P, _I, _I]),
+    "sa_stage": (_I, [_P, _I, _D, _D, _D]),
+    "sa_run": (_I, [_P, _I, _I, _I]),
+    "sa_wait": (_I, [_P]),
+    "sa_fetch": (_I, [_P, _I, _D, ct.POINTER(ct.c_int)]),
+    "sa_run_event_ms": (ct.c_double, [_P]),
+    "sa_profile": (_I, [_P, _I, _I, _I, _D]),
+    "sa_decide": (_I, [_P, _I, ct.POINTER(ct.c_int32)]),
+    "sa_info": (_I, [_P, ct.POINTER(ct.c_int64)]),
+    "sa_device_count": (_I, []),
+    "sa_last_error": (ct.c_char_p, []),
+    "sa_version": (ct.c_char_p, []),
+}
+
+_lib = None
+
+
+class SparcAmpError(RuntimeError):
+    """A non-zero status from libsparc_amp.so."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libsparc_amp error {code}: {msg}")
+        self.code = code
+
+
+def load(path: str = LIB_PATH) -> ct.CDLL:
+    """Load (once) and type the library; raises ImportError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ct.CDLL(path)
+    for name, (res, args) in _SIG.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != SA_OK:
+        msg = load().sa_last_error().decode(errors="replace")
+        if rc == SA_ERR_ARG:
+            raise AssertionError(msg)
+        raise SparcAmpError(rc, msg)
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(_D)
+
+
+def as_f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)

@@ -1,0 +1,246 @@
+"""Monte-Carlo harness around the AMP hot path.
+
+Drop-ins for the reference's per-codeword simulator (plain-SPARC branch of
+``amp_ldpc_sim``, ldpc/sparc_ldpc.py:359-545), its helpers
+(``SPARCParams`` :227-246, ``bits2indices`` :317-341, ``pa_parameterised``
+:172-186) and the BER sweep of ``waterfall``'s plain branch (:1126-1282), plus
+a batched Monte-Carlo driver that keeps the codeword batch on the device and
+shards reps across ranks.
+
+The per-codeword functions consume ``np.random``'s global state in the same
+order as the reference, so a seeded call reproduces the reference's message
+and noise draws exactly.
+"""
+from __future__ import annotations
+
+import math
+import csv
+import os
+
+import numpy as np
+
+from .amp import amp, amp_test
+from .operators import SparcOperator, make_ordering, sparc_transforms, sparc_transforms_shorter
+
+__all__ = [
+    "SPARCParams", "LDPCParams", "pa_parameterised", "bits2indices", "ber_of",
+    "amp_ldpc_sim", "mc_decode", "ebno_to_sigma", "waterfall_plain", "amp_test_reps",
+]
+
+
+class SPARCParams:
+    """sparc_ldpc.py:227-246 (same fields)."""
+
+    def __init__(self, L, M, sigma, p, r, t, a=None, f=None, C=None):
+        self.L = L
+        self.M = M
+        self.sigma = sigma
+        self.p = p
+        self.r = r
+        self.t = t
+        self.a = a
+        self.f = f
+        self.C = C
+
+
+class LDPCParams:
+    """sparc_ldpc.py:250-255 (same fields).  The outer LDPC code is a later
+    row of the build; passing one raises NotImplementedError."""
+
+    def __init__(self, standard, r_ldpc, z, ptype='A'):
+        self.standard = standard
+        self.r_ldpc = r_ldpc
+        self.z = z
+        self.ptype = ptype
+
+
+def pa_parameterised(L, C, P, a, f):
+    """sparc_ldpc.py:172-186: exponential power allocation flattened after fL."""
+    pa = 2 ** (-2 * a * C * np.arange(L) / L)
+    pa[int(f * L):] = pa[int(f * L)]
+    pa /= pa.sum() / P
+    return pa
+
+
+def bits2indices(bits, m):
+    """sparc_ldpc.py:317-341: MSB-first, log2(m) bits per section."""
+    logm = int(math.log(m, 2))
+    assert len(bits) % logm == 0
+    b = np.asarray(bits, dtype=np.int64).reshape(-1, logm)
+    w = 1 << np.arange(logm - 1, -1, -1, dtype=np.int64)
+    return (b * w).sum(axis=1).tolist()
+
+
+_POP8 = np.array([bin(i).count("1") for i in range(256)], dtype=np.int64)
+
+
+def _popcount(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    c = np.zeros(x.shape, dtype=np.int64)
+    while np.any(x):
+        c += _POP8[(x & np.uint64(0xFF)).astype(np.int64)]
+        x >>= np.uint64(8)
+    return c
+
+
+def ber_of(sent, decided, total_bits):
+    """sparc_ldpc.py:462: Σ popcount(sent ^ decided) / total_bits (per row)."""
+    s = np.asarray(sent, dtype=np.int64)
+    d = np.asarray(decided, dtype=np.int64)
+    return _popcount(np.bitwise_xor(s, d)).sum(axis=-1) / total_bits
+
+
+def amp_ldpc_sim(sparcparams: SPARCParams, ldpcparams=None, a=None, f=None, C=None, *,
+                 backend=None, precision=None):
+    """Plain-SPARC branch of sparc_ldpc.py:359-545: one Monte-Carlo rep.
+
+    Returns (ber_amp, None, None, R) like the reference with ldpcparams=None.
+    Draw order of np.random: randint(0, 2, total_bits) (:423-424), then
+    randn(n, 1) (:445).
+    """
+    if ldpcparams is not None:
+        raise NotImplementedError("outer LDPC code: SURVEY §8f next row (not in this build yet)")
+    L, M, P = sparcparams.L, sparcparams.M, sparcparams.p
+    sigma, r_sparc, T = sparcparams.sigma, sparcparams.r, sparcparams.t
+    a, f, C = sparcparams.a, sparcparams.f, sparcparams.C
+    n = int(L * np.log2(M) / r_sparc)
+    logm = np.log2(M)
+    total_bits = int(logm * L)
+    Pl = P / L * np.ones(L) if a is None else pa_parameterised(L, C, P, a, f)
+    bits = np.random.randint(0, 2, int(total_bits)).tolist()
+    idx = bits2indices(bits, M)
+    Ab, Az, ordering = sparc_transforms(L, M, n, backend=backend, precision=precision)
+    β0 = np.zeros((L * M, 1))
+    β0[np.arange(L) * M + np.asarray(idx), 0] = np.sqrt(n * Pl)
+    x = Ab(β0)
+    z = np.random.randn(n, 1) * sigma
+    y = (x + z).reshape(-1, 1)
+    β = amp(y, sigma, Pl, L, M, T, Ab, Az).reshape(-1)
+    rx = β.reshape(L, M).argmax(axis=1)
+    ber_amp = float(ber_of(idx, rx, total_bits))
+    R = (L * logm) / n
+    return ber_amp, None, None, R
+
+
+def mc_decode(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True):
+    """Batched Monte-Carlo reps on one device (SURVEY §8d synthetic inputs).
+
+    Rep with seed s: ``RandomState(s)`` draws the L section indices uniform
+    in [0, M) (same law as random bits -> bits2indices) and then the noise
+    N(0, σ²) (n values).  Encoding x = A β₀ runs on the device (batched Ab).
+    Returns dict of int64 counters: bit_errors, blocks, block_errors, iters,
+    section_errors.
+    """
+    L, M, n = op.L, op.M, op.n
+    logm = int(np.log2(M))
+    Pl = np.asarray(Pl, dtype=np.float64)
+    c = np.sqrt(n * Pl)
+    acc = dict(bit_errors=0, blocks=0, block_errors=0, iters=0, section_errors=0)
+    seeds = list(seeds)
+    for s0 in range(0, len(seeds), batch):
+        chunk = seeds[s0:s0 + batch]
+        B = len(chunk)
+        idx = np.empty((B, L), dtype=np.int64)
+        noise = np.empty((B, n))
+        for i, s in enumerate(chunk):
+            rs = np.random.RandomState(s)
+            idx[i] = rs.randint(0, M, L)
+            noise[i] = rs.randn(n) * sigma
+        beta0 = np.zeros((B, L * M))
+        beta0[np.arange(B)[:, None], np.arange(L)[None, :] * M + idx] = c[None, :]
+        y = op.Ab_batch(beta0) + noise
+        _, iters = op.amp_batch(y, Pl, T, None, early_stop)
+        rx = op.decide(B).astype(np.int64)
+        be = _popcount(np.bitwise_xor(idx, rx)).sum(axis=1)
+        acc["bit_errors"] += int(be.sum())
+        acc["blocks"] += B
+        acc["block_errors"] += int((be > 0).sum())
+        acc["iters"] += int(iters.sum())
+        acc["section_errors"] += int((idx != rx).sum())
+    acc["total_bits_per_block"] = L * logm
+    return acc
+
+
+def ebno_to_sigma(ebno_db, P, R):
+    """waterfall's mapping (sparc_ldpc.py:1184,1199-1200), 20*log10 convention."""
+    ebno = 10 ** (ebno_db / 20)
+    snr = ebno / (1 / (2 * R))
+    return float(np.sqrt(P / snr))
+
+
+def waterfall_plain(L, M, P, R, T, ebno_dbs, min_errors=200, max_blocks=250, csv_filename=None,
+                    batch=64, seed0=0, backend=None, precision=None, rank=0, world=1, allreduce=None):
+    """BER_plain column of waterfall() (sparc_ldpc.py:1126-1282) on the GPU.
+
+    Stopping rule per Eb/N0 point as the reference: keep drawing blocks until
+    ``min_errors`` blocks with errors or ``max_blocks`` blocks (:1217-1245);
+    BER = mean per-block BER (= Σ bit errors / (blocks · bits)).  Reps are
+    sharded over ``world`` ranks (rank r takes seeds ≡ r mod world) and the
+    int64 counters are summed with ``allreduce`` (RCCL via torch.distributed
+    in the multi-GPU harness) once per round of batch·world reps.
+    Writes the reference CSV schema (:1257-1264) when csv_filename is given.
+    """
+    n = int(L * np.log2(M) / R)
+    ordering = make_ordering(L, M, n, 0)
+    op = SparcOperator(L, M, n, ordering, backend, precision)
+    Pl = P / L * np.ones(L)
+    rows = []
+    for pi, ebno_db in enumerate(ebno_dbs):
+        sigma = ebno_to_sigma(ebno_db, P, R)
+        tot = np.zeros(4, dtype=np.int64)  # bit_errors, blocks, block_errors, iters
+        rnd = 0
+        while tot[2] < min_errors and tot[1] < max_blocks:
+            base = seed0 + pi * 10_000_000 + rnd * batch * world
+            seeds = [base + rank + world * i for i in range(batch)]
+            r = mc_decode(op, Pl, sigma, T, seeds, batch=batch)
+            part = np.array([r["bit_errors"], r["blocks"], r["block_errors"], r["iters"]], dtype=np.int64)
+            if allreduce is not None:
+                part = allreduce(part)
+            tot += part
+            rnd += 1
+        ber = tot[0] / (tot[1] * L * np.log2(M))
+        rows.append(dict(EbN0_dB=ebno_db, BER_amp_1=0.0, BER_ldpc=0.0, BER_amp_2=0.0,
+                         BER_ldpc_2=0.0, BER_plain=ber, BER_bpsk=0.0,
+                         blocks=int(tot[1]), block_errors=int(tot[2]), mean_iters=tot[3] / tot[1]))
+    if csv_filename and rank == 0:
+        fields = ['EbN0_dB', 'BER_amp_1', 'BER_ldpc', 'BER_amp_2', 'BER_ldpc_2', 'BER_plain', 'BER_bpsk']
+        with open(csv_filename, 'a', newline='') as fh:
+            wr = csv.DictWriter(fh, fieldnames=fields)
+            wr.writeheader()
+            for row in rows:
+                wr.writerow({k: row[k] for k in fields})
+    return rows
+
+
+def amp_test_reps(L=512, M=512, L_zero=154, P=4, snr_dB=10, r_sparc=1, T=64, repeats=100,
+                  backend=None, precision=None):
+    """The reps loop of amp_test.py:161-253: per rep, hard-init AMP on the
+    first L_zero sections (shortened operator), soft-init AMP with the 0/1
+    β₀, and zero-init AMP; returns the three mean BERs.  Draws come from
+    np.random in the reference's order (:185-200)."""
+    snr = 10 ** (snr_dB / 20)
+    sigma = np.sqrt(P / snr)
+    Pl = P / L * np.ones(L)
+    logm = np.log2(M)
+    total_bits = int(L * logm)
+    n = int(L * np.log2(M) / r_sparc)
+    ber_hard = ber_soft = ber_no_init = 0.0
+    for _ in range(repeats):
+        bits = np.random.randint(0, 2, total_bits).tolist()
+        idx = np.asarray(bits2indices(bits, M))
+        Ab, Az, ordering = sparc_transforms(L, M, n, backend=backend, precision=precision)
+        beta = np.zeros((L * M, 1))
+        beta[np.arange(L) * M + idx, 0] = np.sqrt(n * Pl)
+        x = Ab(beta)
+        y = (x + np.random.randn(n, 1) * sigma).reshape(-1, 1)
+        beta_0 = beta / np.sqrt(n * P / L)
+        beta_0[:L_zero * M] = 0
+        y_new = y - Ab(beta_0)
+        Ab_n, Az_n = sparc_transforms_shorter(L_zero, M, n, ordering, backend=backend, precision=precision)
+        bh = amp(y_new, sigma, Pl[:L_zero], L_zero, M, T, Ab_n, Az_n).reshape(-1)
+        ber_hard += ber_of(idx[:L_zero], bh.reshape(L_zero, M).argmax(1), total_bits)
+        bs = amp(y, sigma, Pl, L, M, T, Ab, Az, beta_0).reshape(-1)
+        ber_soft += ber_of(idx, bs.reshape(L, M).argmax(1), total_bits)
+        bz = amp(y, sigma, Pl, L, M, T, Ab, Az).reshape(-1)
+        ber_no_init += ber_of(idx, bz.reshape(L, M).argmax(1), total_bits)
+    return ber_hard / repeats, ber_soft / repeats, ber_no_init / repeats

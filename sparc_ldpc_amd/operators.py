@@ -1,0 +1,322 @@
+"""Design operators on the MI355X: the drop-in for ldpc/sparc_ldpc.py:32-168.
+
+``sparc_transforms`` / ``sparc_transforms_shorter`` / ``block_sub_fht`` /
+``sub_fht`` keep the reference's names, argument order and return shapes.
+The returned ``Ab``/``Az`` are callable objects (so ``x = Ab(β₀)``,
+sparc_ldpc.py:439, and ``y - Ab(β)``, :514 / amp_exit.py:111, work
+unchanged); each carries the device context that ``amp()`` uses to run the
+whole iteration loop on the GPU.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+from collections import OrderedDict
+
+import numpy as np
+
+from . import _lib
+from ._lib import as_f64, check, dptr
+
+__all__ = [
+    "SparcOperator", "AbOp", "AzOp", "make_ordering", "sub_fht", "block_sub_fht",
+    "sparc_transforms", "sparc_transforms_shorter", "default_device",
+]
+
+_BACKENDS = {"hadamard": _lib.SA_BACKEND_HADAMARD, "dense": _lib.SA_BACKEND_DENSE}
+_PRECS = {"fp32": _lib.SA_PREC_F32, "fp64": _lib.SA_PREC_F64}
+
+# Process-wide defaults; bench/tests override through these env vars or kwargs.
+DEFAULT_BACKEND = os.environ.get("SPARC_AMP_BACKEND", "hadamard")
+DEFAULT_PRECISION = os.environ.get("SPARC_AMP_PRECISION", "fp32")
+
+
+def default_device() -> int:
+    """LOCAL_RANK (one process per GPU) if it names a visible device, else 0."""
+    lib = _lib.load()
+    ndev = lib.sa_device_count()
+    if ndev <= 0:
+        raise _lib.SparcAmpError(_lib.SA_ERR_NO_DEVICE, "no HIP device visible (MI355X required)")
+    env = os.environ.get("SPARC_AMP_DEVICE", os.environ.get("LOCAL_RANK", "0"))
+    d = int(env)
+    return d if 0 <= d < ndev else 0
+
+
+def _w_of(n: int, m: int) -> int:
+    # sparc_ldpc.py:52 / :110
+    return 2 ** int(np.ceil(np.log2(max(m + 1, n + 1))))
+
+
+_ORDER_CACHE: "OrderedDict[tuple, np.ndarray]" = OrderedDict()
+
+
+def make_ordering(L: int, M: int, n: int, seed: int = 0) -> np.ndarray:
+    """The reference's row sub-sampling table (sparc_ldpc.py:107-117).
+
+    Legacy ``RandomState(seed)`` (frozen by NEP 19), a *cumulative* shuffle
+    of ``arange(1, w, uint32)`` per section, first n kept.  Host-side set-up,
+    exactly as in the reference; memoised because every Monte-Carlo rep of
+    the reference rebuilds the same seed-0 table (sparc_ldpc.py:433).
+    """
+    key = (int(L), int(M), int(n), int(seed))
+    hit = _ORDER_CACHE.get(key)
+    if hit is not None:
+        _ORDER_CACHE.move_to_end(key)
+        return hit
+    w = _w_of(n, M)
+    rng = np.random.RandomState(seed)
+    ordering = np.empty((L, n), dtype=np.uint32)
+    idxs = np.arange(1, w, dtype=np.uint32)
+    for ll in range(L):
+        rng.shuffle(idxs)
+        ordering[ll] = idxs[:n]
+    ordering.setflags(write=False)
+    _ORDER_CACHE[key] = ordering
+    while len(_ORDER_CACHE) > 8:
+        _ORDER_CACHE.popitem(last=False)
+    return ordering
+
+
+class SparcOperator:
+    """A device-resident SPARC design operator (one ``sa_ctx``)."""
+
+    def __init__(self, L, M, n, ordering, backend=None, precision=None, device=None):
+        lib = _lib.load()
+        backend = backend or DEFAULT_BACKEND
+        precision = precision or DEFAULT_PRECISION
+        if backend not in _BACKENDS:
+            raise ValueError(f"backend must be one of {sorted(_BACKENDS)}")
+        if precision not in _PRECS:
+            raise ValueError(f"precision must be one of {sorted(_PRECS)}")
+        ordering = np.ascontiguousarray(ordering, dtype=np.uint32)
+        assert ordering.shape == (L, n), "ordering must be (L, n)"
+        self.L, self.M, self.n = int(L), int(M), int(n)
+        self.w = _w_of(self.n, self.M)
+        self.backend, self.precision = backend, precision
+        self.device = default_device() if device is None else int(device)
+        self.ordering = ordering
+        self._ctx = _lib.ct.c_void_p()
+        check(lib.sa_create(_lib.ct.byref(self._ctx), self.L, self.M, self.n,
+                            ordering.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_uint32)),
+                            _BACKENDS[backend], _PRECS[precision], self.device))
+        self._lib = lib
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.value:
+            try:
+                self._lib.sa_destroy(ctx)
+            except Exception:
+                pass
+            self._ctx = None
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    # ---- operator products (fp64 at the boundary) -----------------------
+    def Ab_batch(self, beta: np.ndarray) -> np.ndarray:
+        """A β for a (B, L*M) batch -> (B, n)."""
+        beta = as_f64(beta)
+        B = beta.shape[0]
+        assert beta.size == B * self.L * self.M
+        out = np.empty((B, self.n))
+        check(self._lib.sa_Ab(self._ctx, B, dptr(beta), dptr(out)))
+        return out
+
+    def Az_batch(self, z: np.ndarray) -> np.ndarray:
+        """Aᵀ z for a (B, n) batch -> (B, L*M)."""
+        z = as_f64(z)
+        B = z.shape[0]
+        assert z.size == B * self.n
+        out = np.empty((B, self.L * self.M))
+        check(self._lib.sa_Az(self._ctx, B, dptr(z), dptr(out)))
+        return out
+
+    # ---- AMP -------------------------------------------------------------
+    def amp_batch(self, y, Pl, T, beta0=None, early_stop=True):
+        """Decode B codewords: y (B, n) -> (β̂ (B, L*M), iters (B,)).
+
+        iters[b] is the loop index at which the exact τ == last_τ stop fired
+        (sparc_ldpc.py:204) or T when the loop ran out.
+        """
+        y = as_f64(y)
+        B = y.shape[0] if y.ndim == 2 else 1
+        assert y.size == B * self.n, "y must hold B x n values"
+        Pl = as_f64(Pl).reshape(-1)
+        assert Pl.size == self.L, "Pl must hold L section powers"
+        T = int(T)
+        assert T >= 0
+        b0p = None
+        if beta0 is not None:
+            beta0 = as_f64(beta0)
+            assert beta0.size == B * self.L * self.M, "β₀ must hold L*M values per codeword"
+            b0p = dptr(beta0)
+        out = np.empty((B, self.L * self.M))
+        iters = np.empty(B, dtype=np.int32)
+        flags = 0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP
+        check(self._lib.sa_amp(self._ctx, B, dptr(y), dptr(Pl), T, b0p, dptr(out),
+                               iters.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int)), flags))
+        return out, iters
+
+    def decide(self, B: int) -> np.ndarray:
+        """Section argmax of the last decode (device-side), (B, L) int32."""
+        idx = np.empty((B, self.L), dtype=np.int32)
+        check(self._lib.sa_decide(self._ctx, B, idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
+        return idx
+
+    # ---- device-resident path (bench) -------------------------------------
+    def reserve(self, B, T):
+        check(self._lib.sa_reserve(self._ctx, int(B), int(T)))
+
+    def stage(self, y, Pl=None, beta0=None):
+        y = as_f64(y)
+        B = y.shape[0] if y.ndim == 2 else 1
+        Pl = None if Pl is None else as_f64(Pl)
+        beta0 = None if beta0 is None else as_f64(beta0)
+        check(self._lib.sa_stage(self._ctx, B, dptr(y), None if Pl is None else dptr(Pl),
+                                 None if beta0 is None else dptr(beta0)))
+        return B
+
+    def run(self, B, T, early_stop=True, beta0=False):
+        flags = (0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP) | (_lib.SA_FLAG_BETA0 if beta0 else 0)
+        check(self._lib.sa_run(self._ctx, int(B), int(T), flags))
+
+    def wait(self):
+        check(self._lib.sa_wait(self._ctx))
+
+    def last_run_ms(self) -> float:
+        return float(self._lib.sa_run_event_ms(self._ctx))
+
+    KERNEL_KINDS = ("k_sec", "k_row", "k_dense_az", "k_dense_den", "k_dense_ab")
+
+    def profile(self, B, T, early_stop=True, beta0=False):
+        """Eager decode with per-launch HIP events: {kind: (mean_ms, launches)}, total_ms."""
+        flags = (0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP) | (_lib.SA_FLAG_BETA0 if beta0 else 0)
+        out = np.zeros(11)
+        check(self._lib.sa_profile(self._ctx, int(B), int(T), flags, dptr(out)))
+        kinds = {k: (float(out[2 * i]), int(out[2 * i + 1])) for i, k in enumerate(self.KERNEL_KINDS)}
+        return kinds, float(out[10])
+
+    def fetch(self, B):
+        out = np.empty((B, self.L * self.M))
+        iters = np.empty(B, dtype=np.int32)
+        check(self._lib.sa_fetch(self._ctx, B, dptr(out), iters.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
+        return out, iters
+
+    def info(self):
+        o = np.zeros(8, dtype=np.int64)
+        check(self._lib.sa_info(self._ctx, o.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int64))))
+        keys = ("L", "M", "n", "w", "backend", "precision", "device", "device_bytes")
+        return dict(zip(keys, (int(v) for v in o)))
+
+    def subset(self, sections) -> "SparcOperator":
+        """Operator over the given parent sections (sparc_transforms_shorter)."""
+        sec = np.ascontiguousarray(np.asarray(sections, dtype=np.int64).reshape(-1))
+        return SparcOperator(len(sec), self.M, self.n, self.ordering[sec],
+                             self.backend, self.precision, self.device)
+
+
+class AbOp:
+    """``Ab(β)`` -> A β / (n, 1) float64 (sparc_ldpc.py:143-144)."""
+
+    def __init__(self, op: SparcOperator):
+        self.op = op
+
+    def __call__(self, b):
+        b = np.asarray(b)
+        assert b.size == self.op.L * self.op.M  # block_sub_fht.Ax, sparc_ldpc.py:121
+        return self.op.Ab_batch(b.reshape(1, -1)).reshape(-1, 1)
+
+
+class AzOp:
+    """``Az(z)`` -> Aᵀ z / (L*M, 1) float64 (sparc_ldpc.py:145-146)."""
+
+    def __init__(self, op: SparcOperator):
+        self.op = op
+
+    def __call__(self, z):
+        z = np.asarray(z)
+        assert z.size == self.op.n  # block_sub_fht.Ay, sparc_ldpc.py:129
+        return self.op.Az_batch(z.reshape(1, -1)).reshape(-1, 1)
+
+
+_OP_CACHE: "OrderedDict[tuple, SparcOperator]" = OrderedDict()
+
+
+def _cached_operator(L, M, n, ordering, backend, precision, device):
+    backend = backend or DEFAULT_BACKEND
+    precision = precision or DEFAULT_PRECISION
+    device = default_device() if device is None else int(device)
+    o = np.ascontiguousarray(ordering, dtype=np.uint32)
+    key = (L, M, n, hashlib.sha1(o.tobytes()).hexdigest(), backend, precision, device)
+    op = _OP_CACHE.get(key)
+    if op is None:
+        op = SparcOperator(L, M, n, o, backend, precision, device)
+        _OP_CACHE[key] = op
+        while len(_OP_CACHE) > 6:
+            _OP_CACHE.popitem(last=False)
+    else:
+        _OP_CACHE.move_to_end(key)
+    return op
+
+
+def sparc_transforms(L, M, n, seed=0, *, backend=None, precision=None, device=None):
+    """Drop-in for sparc_ldpc.py:140-147: returns (Ab, Az, ordering)."""
+    ordering = make_ordering(L, M, n, seed)
+    op = _cached_operator(L, M, n, ordering, backend, precision, device)
+    return AbOp(op), AzOp(op), ordering
+
+
+def sparc_transforms_shorter(L, M, n, ordering, *, backend=None, precision=None, device=None):
+    """Drop-in for sparc_ldpc.py:154-168: operator over ``ordering[:L, :]``.
+
+    Callers pass fancy-indexed subsets (amp_exit.py:113-116); any (≥L, n)
+    array works.
+    """
+    ordering = np.asarray(ordering)
+    op = _cached_operator(L, M, n, ordering[:L, :], backend, precision, device)
+    return AbOp(op), AzOp(op)
+
+
+def block_sub_fht(n, m, l, seed=0, ordering=None, *, backend=None, precision=None, device=None):
+    """Drop-in for sparc_ldpc.py:81-136: unscaled (Ax, Ay, ordering).
+
+    The device computes A·x / sqrt(n); Ax/Ay here undo the 1/sqrt(n) so the
+    contract (no scaling) matches the reference.
+    """
+    assert n > 0, "n must be positive"
+    assert m > 0, "m must be positive"
+    assert l > 0, "l must be positive"
+    if ordering is not None:
+        assert ordering.shape == (l, n)
+    else:
+        ordering = make_ordering(l, m, n, seed)
+    op = _cached_operator(l, m, n, ordering, backend, precision, device)
+    s = np.sqrt(n)
+
+    def Ax(x):
+        assert np.asarray(x).size == l * m
+        return op.Ab_batch(np.asarray(x).reshape(1, -1)).reshape(-1) * s
+
+    def Ay(y):
+        assert np.asarray(y).size == n
+        return op.Az_batch(np.asarray(y).reshape(1, -1)).reshape(-1) * s
+
+    return Ax, Ay, ordering
+
+
+def sub_fht(n, m, seed=0, ordering=None, **kw):
+    """Drop-in for sparc_ldpc.py:32-79 (one block): unscaled (Ax, Ay, ordering)."""
+    assert n > 0, "n must be positive"
+    assert m > 0, "m must be positive"
+    if ordering is None:
+        w = _w_of(n, m)
+        rng = np.random.RandomState(seed)
+        idxs = np.arange(1, w, dtype=np.uint32)
+        rng.shuffle(idxs)
+        ordering = idxs[:n]
+    else:
+        assert ordering.shape == (n,)
+    Ax, Ay, _ = block_sub_fht(n, m, 1, ordering=np.asarray(ordering).reshape(1, n), **kw)
+    return Ax, Ay, ordering

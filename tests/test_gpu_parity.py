@@ -1,0 +1,247 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference's golden vectors.
+
+Tolerances (BASELINE.json north_star: "within 1e-5 relative fp32"):
+  * fp32 device precision: ‖x − ref‖₂ / ‖ref‖₂ ≤ 1e-5 and identical section
+    argmax (SURVEY §0.4 — per-element relative error is meaningless for the
+    ~e^-50 saturated entries);
+  * fp64 device precision: ‖x − ref‖₂ / ‖ref‖₂ ≤ 1e-11 (only the summation
+    order differs from the reference's).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import amp_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"fp32": 1e-5, "fp64": 1e-11}
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    b = np.asarray(b, dtype=np.float64).reshape(-1)
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+@pytest.fixture(scope="module")
+def sp(lib_gpu):
+    import sparc_ldpc_amd
+    return sparc_ldpc_amd
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_operator_small_golden(sp, prec):
+    g = golden("small.npz")
+    L, M, n = int(g["L"]), int(g["M"]), int(g["n"])
+    Ab, Az, ordering = sp.sparc_transforms(L, M, n, precision=prec)
+    assert np.array_equal(ordering, g["ordering"])
+    assert rel(Ab(g["brand"]), g["Ab_brand"]) <= TOL[prec]
+    assert rel(Az(g["zrand"]), g["Az_zrand"]) <= TOL[prec]
+    assert Ab(g["brand"]).shape == (n, 1) and Az(g["zrand"]).shape == (L * M, 1)
+    sub = g["sub"]
+    Ab_s, Az_s = sp.sparc_transforms_shorter(len(sub), M, n, ordering[sub], precision=prec)
+    assert rel(Ab_s(g["bsub"]), g["Ab_sub"]) <= TOL[prec]
+    assert rel(Az_s(g["zrand"]), g["Az_sub"]) <= TOL[prec]
+
+
+@pytest.mark.parametrize("L,M,R", [(12, 2, 1.0), (40, 4, 1.0), (16, 64, 1.0), (9, 128, 0.8),
+                                   (6, 256, 1.0), (5, 512, 5 / 6), (3, 1024, 1.0), (2, 4096, 1.0)])
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_operator_sizes_vs_oracle(sp, L, M, R, prec):
+    n = int(L * np.log2(M) / R)
+    Ab, Az, ordering = sp.sparc_transforms(L, M, n, precision=prec)
+    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
+    assert np.array_equal(ordering, oord)
+    rs = np.random.RandomState(L * 1000 + M)
+    b = rs.randn(L * M, 1)
+    z = rs.randn(n, 1)
+    assert rel(Ab(b), oAb(b)) <= TOL[prec]
+    assert rel(Az(z), oAz(z)) <= TOL[prec]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_amp_small_trajectory(sp, prec):
+    g = golden("small.npz")
+    L, M, n, T = int(g["L"]), int(g["M"]), int(g["n"]), int(g["T"])
+    Ab, Az, _ = sp.sparc_transforms(L, M, n, precision=prec)
+    Pl = float(g["P"]) / L * np.ones(L)
+    for t in (1, 2, 3, 5, 8):
+        b = sp.amp(g["y"], 0, Pl, L, M, t, Ab, Az)
+        assert b.shape == (L * M, 1)
+        assert rel(b, g["traj"][t - 1]) <= TOL[prec], t
+    b, t = sp.amp_test(g["y"], 0, Pl, L, M, T, Ab, Az)
+    assert rel(b, g["beta_final"]) <= TOL[prec]
+    assert np.array_equal(orc.section_argmax(b, L, M), orc.section_argmax(g["beta_final"], L, M))
+    b, t = sp.amp_test(g["y"], 0, Pl, L, M, T, Ab, Az, g["beta0_soft"])
+    assert rel(b, g["beta_soft"]) <= TOL[prec]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_c1_reps(sp, prec):
+    g = golden("c1.npz")
+    L, M, n, T = int(g["L"]), int(g["M"]), int(g["n"]), int(g["T"])
+    Ab, Az, _ = sp.sparc_transforms(L, M, n, precision=prec)
+    Pl = float(g["P"]) / L * np.ones(L)
+    for r in range(4):
+        y = g[f"y_{r}"]
+        for k, t in enumerate((1, 2, 5)):
+            assert rel(sp.amp(y, 0, Pl, L, M, t, Ab, Az), g[f"traj_{r}"][k]) <= TOL[prec]
+        b, t = sp.amp_test(y, 0, Pl, L, M, T, Ab, Az)
+        assert np.array_equal(orc.section_argmax(b, L, M), orc.section_argmax(g[f"beta_{r}"], L, M))
+        assert rel(b, g[f"beta_{r}"]) <= TOL[prec]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_c2_golden(sp, prec):
+    """L=M=512 R=1 P=4, snr 10 dB (amp_test.py:161-176), T=64."""
+    g = golden("c2.npz")
+    L, M, n, T = int(g["L"]), int(g["M"]), int(g["n"]), int(g["T"])
+    Ab, Az, _ = sp.sparc_transforms(L, M, n, precision=prec)
+    Pl = float(g["P"]) / L * np.ones(L)
+    y = g["y"]
+    assert rel(sp.amp(y, 0, Pl, L, M, 1, Ab, Az), g["beta_t1"]) <= max(TOL[prec], 1e-7)
+    b, t = sp.amp_test(y, 0, Pl, L, M, T, Ab, Az)
+    assert rel(b, g["beta_final"]) <= max(TOL[prec], 1e-7)
+    assert np.array_equal(orc.section_argmax(b, L, M), g["argmax_final"])
+    # hard and soft initialisation of amp_test.py:202-240
+    Lz = int(g["Lz"])
+    beta = np.zeros((L * M, 1)); beta[np.arange(L) * M + g["idx"], 0] = np.sqrt(n * Pl[0])
+    beta_0 = beta / np.sqrt(n * float(g["P"]) / L); beta_0[:Lz * M] = 0
+    y_new = y - Ab(beta_0)
+    Ab_n, Az_n = sp.sparc_transforms_shorter(Lz, M, n, _ordering(sp, L, M, n), precision=prec)
+    bh, _ = sp.amp_test(y_new, 0, Pl[:Lz], Lz, M, T, Ab_n, Az_n)
+    assert np.array_equal(orc.section_argmax(bh, Lz, M), g["argmax_hard"])
+    assert abs(np.linalg.norm(bh) - float(g["beta_hard_norm"])) <= 1e-5 * float(g["beta_hard_norm"])
+    bs, _ = sp.amp_test(y, 0, Pl, L, M, T, Ab, Az, beta_0)
+    assert np.array_equal(orc.section_argmax(bs, L, M), g["argmax_soft"])
+    assert abs(np.linalg.norm(bs) - float(g["beta_soft_norm"])) <= 1e-5 * float(g["beta_soft_norm"])
+
+
+def _ordering(sp, L, M, n):
+    return sp.make_ordering(L, M, n, 0)
+
+
+def test_c5_decisions(sp):
+    """Plain SPARC L=M=512 R=5/6 at Eb/N0 5.33 dB: the reference's own y
+    (from amp_ldpc_sim's draws) decodes to the reference's decisions."""
+    g = golden("c5_reps.npz")
+    L, M, n, T = int(g["L"]), int(g["M"]), int(g["n"]), int(g["T"])
+    Ab, Az, _ = sp.sparc_transforms(L, M, n, precision="fp64")
+    Ab32, Az32, _ = sp.sparc_transforms(L, M, n, precision="fp32")
+    Pl = float(g["P"]) / L * np.ones(L)
+    for s in range(3):
+        b = sp.amp(g[f"y_{s}"], 0, Pl, L, M, T, Ab, Az)
+        assert np.array_equal(orc.section_argmax(b, L, M), g[f"rx_{s}"])
+        b32 = sp.amp(g[f"y_{s}"], 0, Pl, L, M, T, Ab32, Az32)
+        rx32 = orc.section_argmax(b32, L, M)
+        # fp32 may flip a section whose two largest posteriors tie to ~1e-7
+        assert (rx32 != g[f"rx_{s}"]).sum() <= 1
+        assert abs(sp.ber_of(g[f"idx_{s}"], rx32, L * 9) - float(g[f"ber_{s}"])) <= 9 / (L * 9)
+
+
+def test_harness_draws_match_reference(sp):
+    """amp_ldpc_sim consumes np.random like the reference (sparc_ldpc.py:423-446)."""
+    g = golden("c5_reps.npz")
+    L, M, T = int(g["L"]), int(g["M"]), int(g["T"])
+    np.random.seed(1)
+    ber, _, _, R = sp.amp_ldpc_sim(sp.SPARCParams(L, M, float(g["sigma"]), float(g["P"]), float(g["R"]), T),
+                                   precision="fp64")
+    assert abs(ber - float(g["ber_1"])) <= 9 / (L * 9)
+    assert abs(R - L * 9 / int(g["n"])) < 1e-12
+
+
+def test_amp_edge_cases(sp):
+    g = golden("small.npz")
+    L, M, n = int(g["L"]), int(g["M"]), int(g["n"])
+    Ab, Az, _ = sp.sparc_transforms(L, M, n)
+    Pl = float(g["P"]) / L * np.ones(L)
+    y = g["y"]
+    # T = 0: the loop never runs
+    assert np.array_equal(sp.amp(y, 0, Pl, L, M, 0, Ab, Az), np.zeros((L * M, 1)))
+    b0 = g["beta0_soft"]
+    assert np.allclose(sp.amp(y, 0, Pl, L, M, 0, Ab, Az, b0), b0.reshape(-1, 1))
+    # the reference's default sentinel and None both mean "zero start"
+    a1 = sp.amp(y, 0, Pl, L, M, 4, Ab, Az, np.array([None]))
+    a2 = sp.amp(y, 0, Pl, L, M, 4, Ab, Az)
+    a3 = sp.amp(y, 0, Pl, L, M, 4, Ab, Az, np.zeros((L * M, 1)))
+    assert np.array_equal(a1, a2) and np.allclose(a2, a3, rtol=0, atol=1e-6)
+    # y (n,) and (n, 1) are the same
+    assert np.array_equal(sp.amp(y.reshape(-1), 0, Pl, L, M, 4, Ab, Az), a2)
+    # y == 0: tau == last_tau == 0 at t = 0 -> returns the zero start
+    bz, t = sp.amp_test(np.zeros(n), 0, Pl, L, M, 10, Ab, Az)
+    assert t == 0 and not np.any(bz)
+    # bad sizes raise AssertionError like the reference
+    with pytest.raises(AssertionError):
+        Ab(np.zeros(L * M + 1))
+    with pytest.raises(AssertionError):
+        Az(np.zeros(n - 1))
+    with pytest.raises(AssertionError):
+        sp.amp(np.zeros(n + 1), 0, Pl, L, M, 3, Ab, Az)
+    # foreign callables are rejected, never run on the CPU
+    with pytest.raises(TypeError):
+        sp.amp(y, 0, Pl, L, M, 3, lambda b: b, lambda z: z)
+    # bad orderings are rejected by the library
+    bad = np.tile(np.arange(1, n + 1, dtype=np.uint32), (L, 1))
+    bad[0, 1] = bad[0, 0]
+    with pytest.raises(sp.SparcAmpError):
+        sp.SparcOperator(L, M, n, bad)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_batch_equals_single_and_deterministic(sp, prec):
+    L, M, P, R, T = 64, 64, 2.0, 1.0, 20
+    n = int(L * np.log2(M) / R)
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=prec)
+    Pl = P / L * np.ones(L)
+    Ab, _, _ = orc.sparc_transforms(L, M, n)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.6, Ab, 50 + i)[1].reshape(-1) for i in range(5)])
+    bb, it = op.amp_batch(ys, Pl, T)
+    for i in range(5):
+        b1, i1 = op.amp_batch(ys[i:i + 1], Pl, T)
+        assert np.array_equal(b1[0], bb[i]) and i1[0] == it[i]
+    bb2, it2 = op.amp_batch(ys, Pl, T)
+    assert np.array_equal(bb, bb2) and np.array_equal(it, it2)
+
+
+def test_dense_backend_matches_hadamard(sp):
+    for (L, M, R) in [(16, 8, 1.0), (24, 512, 1.0), (64, 64, 5 / 6)]:
+        n = int(L * np.log2(M) / R)
+        Abh, Azh, _ = sp.sparc_transforms(L, M, n, backend="hadamard", precision="fp64")
+        Abd, Azd, _ = sp.sparc_transforms(L, M, n, backend="dense")
+        rs = np.random.RandomState(1)
+        b = rs.randn(L * M, 1); z = rs.randn(n, 1)
+        assert rel(Abd(b), Abh(b)) <= 1e-5
+        assert rel(Azd(z), Azh(z)) <= 1e-5
+        Pl = 2.0 / L * np.ones(L)
+        oAb, _, _ = orc.sparc_transforms(L, M, n)
+        _, y = orc.rep_inputs(L, M, n, Pl, 0.5, oAb, 7)
+        bh = sp.amp(y, 0, Pl, L, M, 12, Abh, Azh)
+        bd = sp.amp(y, 0, Pl, L, M, 12, Abd, Azd)
+        assert rel(bd, bh) <= 1e-5
+        assert np.array_equal(orc.section_argmax(bd, L, M), orc.section_argmax(bh, L, M))
+
+
+def test_full_size_properties_c4(sp):
+    """L=768 M=512 R=5/6 (n=8294): size-independent properties at full size —
+    linearity and adjointness of the operator, and an encode -> channel ->
+    decode round trip that recovers every section at high SNR."""
+    L, M, P = 768, 512, 1.8
+    n = int(L * np.log2(M) / (5 / 6))
+    Ab, Az, _ = sp.sparc_transforms(L, M, n)
+    rs = np.random.RandomState(5)
+    x1, x2 = rs.randn(L * M, 1), rs.randn(L * M, 1)
+    z = rs.randn(n, 1)
+    assert rel(Ab(2.5 * x1 + x2), 2.5 * Ab(x1) + Ab(x2)) <= 1e-5
+    lhs = float((Ab(x1) * z).sum()); rhs = float((x1 * Az(z)).sum())
+    assert abs(lhs - rhs) <= 1e-4 * (abs(lhs) + 1e-3 * np.linalg.norm(x1) * np.linalg.norm(z))
+    Pl = P / L * np.ones(L)
+    idx = rs.randint(0, M, L)
+    b0 = np.zeros((L * M, 1)); b0[np.arange(L) * M + idx, 0] = np.sqrt(n * Pl)
+    y = Ab(b0) + 0.3 * rs.randn(n, 1)
+    b, t = sp.amp_test(y, 0.3, Pl, L, M, 64, Ab, Az)
+    assert np.array_equal(orc.section_argmax(b, L, M), idx)
+    # β̂ is a per-section posterior scaled by sqrt(n Pl): rows sum to that
+    assert np.allclose(b.reshape(L, M).sum(1), np.sqrt(n * Pl), rtol=1e-4)

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 LIB_NAME = "libsparc_amp.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("SPARC_AMP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 SA_OK = 0
 SA_ERR_ARG = -1

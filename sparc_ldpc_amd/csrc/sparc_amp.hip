@@ -77,26 +77,91 @@ __device__ __forceinline__ int elem_index(int lane, int i) {
   return (i / Q) * (64 * Q) + lane * Q + (i % Q);
 }
 
+// Cross-lane partner x[lane ^ m] for constant m, all on the VALU:
+// xor 1/2: DPP quad_perm; xor 4/8: DPP row_shl/row_shr by m selected by lane
+// bit (the shifted-in out-of-row lanes are never selected); xor 16/32:
+// v_permlane16_swap / v_permlane32_swap (gfx950).  Doubles move as halves.
+template <int m>
+__device__ __forceinline__ int xor_lane_i32(int x) {
+  if constexpr (m == 1) {
+    return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (m == 2) {
+    return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (m == 4 || m == 8) {
+    const int up = __builtin_amdgcn_mov_dpp(x, 0x100 + m, 0xF, 0xF, false);  // row_shl:m  (lane + m)
+    const int dn = __builtin_amdgcn_mov_dpp(x, 0x110 + m, 0xF, 0xF, false);  // row_shr:m  (lane - m)
+    return (threadIdx.x & m) ? dn : up;
+  } else if constexpr (m == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    static_assert(m == 32, "xor mask");
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
+  }
+}
+
+template <int m, typename real>
+__device__ __forceinline__ real xor_lane(real x) {
+  if constexpr (sizeof(real) == 4) {
+    return __int_as_float(xor_lane_i32<m>(__float_as_int(x)));
+  } else {
+    const long long u = __double_as_longlong(x);
+    const int lo = xor_lane_i32<m>((int)(u & 0xffffffffLL));
+    const int hi = xor_lane_i32<m>((int)(u >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  }
+}
+
+// One lane-bit butterfly stage: lower lane x + p, upper lane p - x, as a
+// single fma with the per-lane sign (+1 lower, -1 upper).
+template <int m, typename real, int E>
+__device__ __forceinline__ void lane_butterfly(real (&x)[E], int lane) {
+  const real sg = (lane & m) ? (real)-1 : (real)1;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const real p = xor_lane<m>(x[i]);
+    x[i] = fma(x[i], sg, p);
+  }
+}
+
+// Full-wave xor-butterfly reductions (fixed order: deterministic bits).
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  v += xor_lane<32>(v);
+  v += xor_lane<16>(v);
+  v += xor_lane<8>(v);
+  v += xor_lane<4>(v);
+  v += xor_lane<2>(v);
+  v += xor_lane<1>(v);
   return v;
 }
 
 template <typename T>
+__device__ __forceinline__ void wave_sum2(T& a, T& b) {
+  a += xor_lane<32>(a); b += xor_lane<32>(b);
+  a += xor_lane<16>(a); b += xor_lane<16>(b);
+  a += xor_lane<8>(a); b += xor_lane<8>(b);
+  a += xor_lane<4>(a); b += xor_lane<4>(b);
+  a += xor_lane<2>(a); b += xor_lane<2>(b);
+  a += xor_lane<1>(a); b += xor_lane<1>(b);
+}
+
+template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    T o = __shfl_xor(v, m);
-    v = o > v ? o : v;
-  }
+  T o;
+  o = xor_lane<32>(v); v = o > v ? o : v;
+  o = xor_lane<16>(v); v = o > v ? o : v;
+  o = xor_lane<8>(v); v = o > v ? o : v;
+  o = xor_lane<4>(v); v = o > v ? o : v;
+  o = xor_lane<2>(v); v = o > v ? o : v;
+  o = xor_lane<1>(v); v = o > v ? o : v;
   return v;
 }
 
 // In-wave natural-order Walsh-Hadamard transform of one section.
 // Butterfly (a, b) -> (a + b, a - b) on every index bit: register bits first,
-// then lane bits via cross-lane xor shuffles.
+// then lane bits (only the first log2(mlanes) lane bits when M < 64).
 template <typename real, int E>
 __device__ __forceinline__ void fwht_wave(real (&x)[E], int lane, int mlanes) {
 #pragma unroll
@@ -110,14 +175,12 @@ __device__ __forceinline__ void fwht_wave(real (&x)[E], int lane, int mlanes) {
       }
     }
   }
-  for (int m = 1; m < mlanes; m <<= 1) {
-    const bool up = (lane & m) != 0;
-#pragma unroll
-    for (int i = 0; i < E; ++i) {
-      real p = __shfl_xor(x[i], m);
-      x[i] = up ? (p - x[i]) : (x[i] + p);
-    }
-  }
+  if (mlanes > 1) lane_butterfly<1>(x, lane);
+  if (mlanes > 2) lane_butterfly<2>(x, lane);
+  if (mlanes > 4) lane_butterfly<4>(x, lane);
+  if (mlanes > 8) lane_butterfly<8>(x, lane);
+  if (mlanes > 16) lane_butterfly<16>(x, lane);
+  if (mlanes > 32) lane_butterfly<32>(x, lane);
 }
 
 template <typename real> __device__ __forceinline__ real dsqrt(real x);
@@ -159,34 +222,36 @@ __device__ __forceinline__ void store_section(real* p, const real (&x)[E], int l
 // independent of m, and the per-section max cannot underflow a section.
 template <typename real, int E>
 __device__ __forceinline__ real denoise_section(real (&v)[E], const real (&bprev)[E], real* beta_l,
-                                                int lane, int M, real cl, real tau2, real sqrt_n) {
+                                                int lane, int M, real cl, real tau2, real sqrt_n,
+                                                bool store = true) {
+  // u = (beta + Az/sqrt(n)) * sqrt(n Pl) / tau^2 with the two divisions of
+  // :213/:215 folded into one per-section scale
+  const real inv_sn = (real)1 / sqrt_n;
+  const real k = cl / tau2;
   real u[E];
   real mx = neg_inf<real>();
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const int e = elem_index<E>(lane, i);
-    const real s = bprev[i] + v[i] / sqrt_n;       // :213
-    const real uu = s * cl / tau2;                 // :215
+    const real s = fma(v[i], inv_sn, bprev[i]);   // :213
+    const real uu = s * k;                          // :215
     u[i] = e < M ? uu : neg_inf<real>();
     mx = u[i] > mx ? u[i] : mx;
   }
-  mx = wave_max(mx);                               // :216 (per section)
-  real S = 0;
+  mx = wave_max(mx);                                // :216 (per section)
+  real S = 0, S2 = 0;
 #pragma unroll
   for (int i = 0; i < E; ++i) {
-    u[i] = dexp<real>(u[i] - mx);                  // :217; exp(-inf) = 0 on idle lanes
+    u[i] = dexp<real>(u[i] - mx);                   // :217; exp(-inf) = 0 on idle lanes
     S += u[i];
+    S2 += u[i] * u[i];
   }
-  S = wave_sum(S);                                 // :218
-  real bb = 0;
+  wave_sum2(S, S2);                                 // :218 and sum(beta^2) together
+  const real scale = cl / S;                        // :219
 #pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const real bn = cl * u[i] / S;                 // :219
-    v[i] = bn;
-    bb += bn * bn;
-  }
-  store_section<real, E>(beta_l, v, lane, M);
-  return wave_sum(bb);
+  for (int i = 0; i < E; ++i) v[i] = u[i] * scale;
+  if (store) store_section<real, E>(beta_l, v, lane, M);
+  return S2 * scale * scale;                        // sum(beta^2) over the section
 }
 
 // Q-wide vector load / store of one wave's section elements (E per lane).
@@ -246,6 +311,8 @@ struct SecArgs {
   real* __restrict__ tau;            // [B][T1]
   int* __restrict__ iters;           // [B]
   int L, M, n, w, nhi, G, NZ, T1, t, mode, early_stop;
+  int RS;  // row splits: RS workgroups share a section group, each gathers n/RS rows of Ab
+  int B, NC;  // batched kernel: codewords, codeword chunks of CB
   real sqrt_n;
 };
 
@@ -308,13 +375,33 @@ __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
 // workgroup gathers its 4 sections' contributions to every row of Ab into
 // abp[b][g][:].  Loads independent of z (bucket table, previous beta) are
 // issued before the z barrier so their latency overlaps.
+#ifdef SA_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP(i)                                                                        \
+  do {                                                                                  \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                       \
+      __builtin_amdgcn_sched_barrier(0);                                                \
+      unsigned long long _t;                                                            \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");       \
+      g_stamps[i] = _t;                                                                 \
+      __builtin_amdgcn_sched_barrier(0);                                                \
+    }                                                                                   \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
+
 template <typename real, int E>
 __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
+  STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int KH = E >= 16 ? 2 : (E >= 8 ? 16 : 16);
   constexpr int NQ = (E + 3) / 4;
   constexpr int KR = 8;  // rows per thread whose Ab-table loads are in flight together
-  const int g = blockIdx.x, b = blockIdx.y;
+  const int g = blockIdx.x / a.RS, rsi = blockIdx.x % a.RS, b = blockIdx.y;
+  const int rows_per = (a.n + a.RS - 1) / a.RS;
+  const int rb0 = rsi * rows_per, rb1 = min(a.n, rb0 + rows_per);
+  const bool owner = rsi == 0;  // writes beta / beta^2 / tau for the group
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int M = a.M, n = a.n;
   const size_t LM = (size_t)a.L * M;
@@ -340,8 +427,8 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     load_section<real, E>(bl, v, lane, M);
 #pragma unroll
     for (int u = 0; u < KR; ++u) {
-      const int r = u * 256 + tid;
-      f[u] = fw[r < n ? r : 0];
+      const int r = rb0 + u * 256 + tid;
+      f[u] = fw[r < rb1 ? r : 0];
     }
   } else {
     // Every load that does not depend on z is issued together with the z
@@ -365,8 +452,8 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     if (a.mode == SEC_AMP) {
 #pragma unroll
       for (int u = 0; u < KR; ++u) {
-        const int r = u * 256 + tid;
-        f[u] = fw[r < n ? r : 0];
+        const int r = rb0 + u * 256 + tid;
+        f[u] = fw[r < rb1 ? r : 0];
       }
     }
     real tau2 = 1;
@@ -374,13 +461,14 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
       const real tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, n);
       const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
       const bool stop = a.early_stop && (tau == last);
-      if (g == 0 && tid == 0) {
+      if (blockIdx.x == 0 && tid == 0) {
         a.tau[(size_t)b * a.T1 + a.t] = tau;
         if (stop && a.iters[b] < 0) a.iters[b] = a.t;
       }
       if (stop) return;  // uniform over the grid row: beta, z stay as they are
       tau2 = tau * tau;
     }
+    STAMP(1);
     for (int i0 = 0; i0 < nfull; i0 += 256 * 4) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) reinterpret_cast<vec_t*>(zs)[i0 + u * 256 + tid] = t4[u];
@@ -392,6 +480,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     for (int i = nfull * V + tid; i < n; i += 256) zs[i] = zb[i];
     if (tid == 0) zs[n] = 0;
     __syncthreads();
+  STAMP(2);
 
 #pragma unroll
     for (int i = 0; i < E; ++i) v[i] = 0;
@@ -407,9 +496,11 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
           for (int j = 0; j < NQ; ++j) tb[hh][j] = tn[hh][j];
       }
     }
+  STAMP(3);
     fwht_wave<real, E>(v, lane, mlanes);
+  STAMP(4);
     if (a.mode == SEC_AZ) {
-      if (have) {
+      if (have && owner) {
         real* ol = a.out + (size_t)b * LM + (size_t)l * M;
 #pragma unroll
         for (int i = 0; i < E; ++i) v[i] = v[i] / a.sqrt_n;
@@ -418,12 +509,14 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
       return;  // uniform: no barrier follows in this mode
     }
     if (have) {
-      const real bb = denoise_section<real, E>(v, bprev, bl, lane, M, cl, tau2, a.sqrt_n);
+      const real bb = denoise_section<real, E>(v, bprev, bl, lane, M, cl, tau2, a.sqrt_n, owner);
       if (lane == 0) bbw[wv] = bb;  // per-wave beta^2, summed below in section order
+  STAMP(5);
     }
   }
   if (have) {
     fwht_wave<real, E>(v, lane, mlanes);  // T_l = H_M beta_l
+  STAMP(6);
   } else {
 #pragma unroll
     for (int i = 0; i < E; ++i) v[i] = 0;  // missing section of the last group
@@ -438,19 +531,20 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     }
   }
   __syncthreads();
-  if (a.mode == SEC_AMP && tid == 0)
+  STAMP(7);
+  if (a.mode == SEC_AMP && tid == 0 && owner)
     a.bbp[(size_t)b * a.G + g] = ((bbw[0] + bbw[1]) + bbw[2]) + bbw[3];
-  // Ab partial of this group's 4 sections for every row: one 8-B table load
-  // per row (the 4 sections' (k, sign) of that row).
+  // Ab partial of this group's 4 sections for this workgroup's rows: one
+  // 8-B table load per row (the 4 sections' (k, sign) of that row).
   real* abp = a.abp + ((size_t)b * a.G + g) * n;
-  for (int r0 = 0; r0 < n; r0 += 256 * KR) {
+  for (int r0 = rb0; r0 < rb1; r0 += 256 * KR) {
     ushort4 fn[KR];
-    const bool more = r0 + 256 * KR < n;
+    const bool more = r0 + 256 * KR < rb1;
     if (more) {
 #pragma unroll
       for (int u = 0; u < KR; ++u) {
         const int r = r0 + 256 * KR + u * 256 + tid;
-        fn[u] = fw[r < n ? r : 0];
+        fn[u] = fw[r < rb1 ? r : 0];
       }
     }
     real acc[KR];
@@ -469,13 +563,305 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
 #pragma unroll
     for (int u = 0; u < KR; ++u) {
       const int r = r0 + u * 256 + tid;
-      if (r < n) abp[r] = acc[u];
+      if (r < rb1) abp[r] = acc[u];
     }
     if (more) {
 #pragma unroll
       for (int u = 0; u < KR; ++u) f[u] = fn[u];
     }
   }
+#ifdef SA_STAMPS
+  STAMP(8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(9);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Batched section kernel (B codewords share the operator)
+// ---------------------------------------------------------------------------
+// One workgroup = 4 wavefronts x CB codewords, sweeping kSG = 16 consecutive
+// sections in 4 rounds of 4.  z of the CB codewords is staged interleaved
+// ([row][CB]) so one LDS gather fetches the same row of every codeword
+// (ds_read_b64 for CB = 2 fp32); the staged T_l = H_M beta_l are interleaved
+// the same way ([section][k][CB]); the Ab contributions of all 16 sections are
+// accumulated per row in LDS and written once (G = L / 16 partials).  The
+// bucket / Ab tables are read once per workgroup for CB codewords, and all
+// workgroups of a section group are placed on one XCD (blockIdx % 8 labels
+// the XCD) so the group's tables stay in that XCD's L2.
+constexpr int kSG = 16;  // fwd table padding (sections)
+constexpr int kWB = 8;   // sections (waves) per batched workgroup
+
+template <typename real, int CB>
+struct cbvec;
+template <> struct cbvec<float, 1> { using t = float; };
+template <> struct cbvec<float, 2> { using t = float2; };
+template <> struct cbvec<float, 4> { using t = float4; };
+template <> struct cbvec<double, 1> { using t = double; };
+template <> struct cbvec<double, 2> { using t = double2; };
+
+template <typename real, int CB>
+__device__ __forceinline__ void vload(const real* p, real (&o)[CB]) {
+  using V = typename cbvec<real, CB>::t;
+  const V t = *reinterpret_cast<const V*>(p);
+  if constexpr (CB == 1) {
+    o[0] = t;
+  } else if constexpr (CB == 2) {
+    o[0] = t.x; o[1] = t.y;
+  } else {
+    o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = t.w;
+  }
+}
+template <typename real, int CB>
+__device__ __forceinline__ void vstore(real* p, const real (&o)[CB]) {
+  using V = typename cbvec<real, CB>::t;
+  V t;
+  if constexpr (CB == 1) {
+    t = o[0];
+  } else if constexpr (CB == 2) {
+    t.x = o[0]; t.y = o[1];
+  } else {
+    t.x = o[0]; t.y = o[1]; t.z = o[2]; t.w = o[3];
+  }
+  *reinterpret_cast<V*>(p) = t;
+}
+
+template <typename real, int E, int CB, int W>
+__global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NT = W * 64;
+  constexpr int NQ = (E + 3) / 4;
+  constexpr int KH = E >= 16 ? 2 : 4;   // bucket h-steps whose table loads are in flight together
+  constexpr int KR = 3;                 // rows per thread whose Ab-table loads are in flight together
+  constexpr int W4 = W / 4;             // 4-section table groups per workgroup
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int M = a.M, n = a.n;
+  const size_t LM = (size_t)a.L * M;
+  const int mlanes = M < 64 ? M : 64;
+  STAMP(0);
+
+  // XCD-grouped work mapping (speed only: any placement is correct)
+  int g, chunk;
+  {
+    const int bid = blockIdx.x, total = a.G * a.NC;
+    if ((a.G & 7) == 0 && (total & 7) == 0) {
+      const int x = bid & 7, j = bid >> 3;
+      g = (j / a.NC) * 8 + x;
+      chunk = j % a.NC;
+    } else {
+      g = bid / a.NC;
+      chunk = bid % a.NC;
+    }
+  }
+  int bc[CB];
+  bool valid[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const int b = chunk * CB + c;
+    valid[c] = b < a.B;
+    bc[c] = valid[c] ? b : a.B - 1;
+  }
+  const int l = g * W + wv;
+  const bool have = l < a.L;
+  const int lc = have ? l : a.L - 1;
+
+  real* zs = reinterpret_cast<real*>(smem);  // [(n+1)][CB]
+  const int zslots = (((n + 1) * CB * (int)sizeof(real) + 15) / 16 * 16) / (int)sizeof(real);
+  real* ts = zs + zslots;                    // [W][M][CB]
+  real* bbw = ts + (size_t)W * M * CB;       // [W][CB]
+
+  // ---- every load independent of z in flight together ---------------------
+  // z rows of the CB codewords (first pass of the staging loop)
+  constexpr int KZ = 4;
+  real zr[KZ][CB];
+#pragma unroll
+  for (int u = 0; u < KZ; ++u) {
+    const int r = u * NT + tid;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) zr[u][c] = a.z[(size_t)bc[c] * n + (r < n ? r : 0)];
+  }
+  const uint16_t* il = a.inv + (size_t)lc * a.w;
+  ushort4 tb[KH][NQ];
+  load_buckets<E, KH>(il, 0, a.nhi, M, lane, tb);
+  real bprev[CB][E];
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+    load_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lane, M);
+  const real cl = a.c[lc];
+  const ushort4* fw = a.fwd + (size_t)g * W4 * n;
+  ushort4 f[KR][W4];
+#pragma unroll
+  for (int u = 0; u < KR; ++u) {
+    const int r = u * NT + tid;
+#pragma unroll
+    for (int q = 0; q < W4; ++q) f[u][q] = fw[(size_t)q * n + (r < n ? r : 0)];
+  }
+  // tau per codeword (sparc_ldpc.py:203-209)
+  bool live[CB];
+  bool any = false;
+  real tau2[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const real tau = tau_from_parts(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
+    const real last = a.t > 0 ? a.tau[(size_t)bc[c] * a.T1 + a.t - 1] : (real)0;
+    const bool stop = a.early_stop && (tau == last);
+    if (valid[c] && g == 0 && tid == 0) {
+      a.tau[(size_t)bc[c] * a.T1 + a.t] = tau;
+      if (stop && a.iters[bc[c]] < 0) a.iters[bc[c]] = a.t;
+    }
+    live[c] = valid[c] && !stop;
+    any |= live[c];
+    tau2[c] = tau * tau;
+  }
+  if (!any) return;  // uniform
+  STAMP(1);
+
+  // ---- z -> LDS interleaved [row][CB] ------------------------------------
+  for (int r0 = 0; r0 < n; r0 += KZ * NT) {
+#pragma unroll
+    for (int u = 0; u < KZ; ++u) {
+      const int r = r0 + u * NT + tid;
+      if (r < n) vstore<real, CB>(zs + (size_t)r * CB, zr[u]);
+    }
+    if (r0 + KZ * NT < n) {
+#pragma unroll
+      for (int u = 0; u < KZ; ++u) {
+        const int r = r0 + KZ * NT + u * NT + tid;
+#pragma unroll
+        for (int c = 0; c < CB; ++c) zr[u][c] = a.z[(size_t)bc[c] * n + (r < n ? r : 0)];
+      }
+    }
+  }
+  if (tid < CB) zs[(size_t)n * CB + tid] = 0;
+  __syncthreads();
+  STAMP(2);
+
+  // ---- bucket gather of the CB codewords (one LDS access per row index) ----
+  real v[CB][E];
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[c][i] = 0;
+  {
+    constexpr int Q = E < 4 ? E : 4;
+    for (int h0 = 0; h0 < a.nhi; h0 += KH) {
+      ushort4 tn[KH][NQ];
+      const bool more = h0 + KH < a.nhi;
+      if (more) load_buckets<E, KH>(il, h0 + KH, a.nhi, M, lane, tn);
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh) {
+        if (h0 + hh < a.nhi) {
+          const bool neg = __popc(h0 + hh) & 1;  // sgn(h): high index bits of w-M+c all ones
+#pragma unroll
+          for (int i = 0; i < E; i += Q) {
+            const ushort4 r4 = tb[hh][i / Q];
+            const unsigned short rr4[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+              real zz[CB];
+              vload<real, CB>(zs + (size_t)rr4[q] * CB, zz);
+#pragma unroll
+              for (int c = 0; c < CB; ++c) v[c][i + q] += neg ? -zz[c] : zz[c];
+            }
+          }
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int hh = 0; hh < KH; ++hh)
+#pragma unroll
+          for (int j = 0; j < NQ; ++j) tb[hh][j] = tn[hh][j];
+      }
+    }
+  }
+  STAMP(3);
+  real bbl[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    fwht_wave<real, E>(v[c], lane, mlanes);
+    real* bl = a.beta + (size_t)bc[c] * LM + (size_t)lc * M;
+    bbl[c] = denoise_section<real, E>(v[c], bprev[c], bl, lane, M, cl, tau2[c], a.sqrt_n, have && live[c]);
+    if (have) {
+      fwht_wave<real, E>(v[c], lane, mlanes);  // T_l = H_M beta_l
+    } else {
+      bbl[c] = 0;
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[c][i] = 0;
+    }
+  }
+  STAMP(4);
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = elem_index<E>(lane, i);
+    if (e < M) {
+      real o[CB];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) o[c] = v[c][i];
+      vstore<real, CB>(ts + ((size_t)wv * M + e) * CB, o);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c) bbw[wv * CB + c] = bbl[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    if (tid == c && live[c]) {
+      real t = 0;
+      for (int w2 = 0; w2 < W; ++w2) t += bbw[w2 * CB + c];
+      a.bbp[(size_t)bc[c] * a.G + g] = t;
+    }
+  }
+  STAMP(5);
+  // ---- Ab partial of the workgroup's W sections for every row ---------------
+  for (int r0 = 0; r0 < n; r0 += KR * NT) {
+    ushort4 fn[KR][W4];
+    const bool more = r0 + KR * NT < n;
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        const int r = r0 + KR * NT + u * NT + tid;
+#pragma unroll
+        for (int q = 0; q < W4; ++q) fn[u][q] = fw[(size_t)q * n + (r < n ? r : 0)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      const int r = r0 + u * NT + tid;
+      real acc[CB];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) acc[c] = 0;
+#pragma unroll
+      for (int q = 0; q < W4; ++q) {
+        const unsigned ff[4] = {f[u][q].x, f[u][q].y, f[u][q].z, f[u][q].w};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          real t[CB];
+          vload<real, CB>(ts + ((size_t)(q * 4 + s4) * M + (ff[s4] & 0x7fffu)) * CB, t);
+          const bool ng = ff[s4] & 0x8000u;
+#pragma unroll
+          for (int c = 0; c < CB; ++c) acc[c] += ng ? -t[c] : t[c];
+        }
+      }
+      if (r < n) {
+#pragma unroll
+        for (int c = 0; c < CB; ++c)
+          if (live[c]) a.abp[((size_t)bc[c] * a.G + g) * n + r] = acc[c];
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < KR; ++u)
+#pragma unroll
+        for (int q = 0; q < W4; ++q) f[u][q] = fn[u][q];
+    }
+  }
+#ifdef SA_STAMPS
+  STAMP(6);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(7);
+#endif
 }
 
 template <typename real>
@@ -809,6 +1195,9 @@ struct sa_ctx {
   Prof* prof = nullptr;
   int L = 0, M = 0, n = 0, w = 0, nhi = 0, backend = 0, prec = 0, device = 0;
   int G = 0, NZ = 0, E = 1;
+  int n_cus = 256;
+  int Gb = 0, CB = 0;  // batched kernel: groups of kSG sections, codewords per workgroup (0 = off)
+  size_t secb_lds = 0;
   int RS = 1, KS = 1, Gd = 0;  // dense splits; Gd = dense denoiser groups
   size_t lda = 0;
   size_t sec_lds = 0;
@@ -877,7 +1266,8 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   const int nT = T > c->Tcap ? T : c->Tcap;
   free_workspace(c);
   const size_t s = rsz(c), LM = (size_t)c->L * c->M;
-  const int Gmax = c->G > c->KS ? c->G : c->KS;
+  int Gmax = c->G > c->KS ? c->G : c->KS;
+  if (c->Gb > Gmax) Gmax = c->Gb;
   int rc;
   if ((rc = dev_alloc(c, &c->d_y, nB * c->n * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_z, nB * c->n * s))) return rc;
@@ -945,18 +1335,20 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
   a.L = c->L; a.M = c->M; a.n = c->n; a.w = c->w; a.nhi = c->nhi; a.G = c->G; a.NZ = c->NZ;
   a.T1 = c->Tcap + 1; a.t = t; a.mode = mode; a.early_stop = early_stop;
+  a.RS = 1;
+  a.B = 0; a.NC = 0;
   a.sqrt_n = (real)std::sqrt((double)c->n);
   return a;
 }
 
 template <typename real>
-RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G) {
+RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb) {
   RowArgs<real> a;
   a.y = (const real*)c->d_y; a.z = (real*)c->d_z; a.abp = (const real*)c->d_abp;
   a.bbp = (const real*)c->d_bbp; a.zzp = (real*)c->d_zzp; a.tau = (const real*)c->d_tau;
   a.out = (real*)c->d_out;
   a.n = c->n; a.G = G; a.NZ = c->NZ;
-  a.Gb = c->backend == SA_BACKEND_DENSE ? c->Gd : c->G; a.T1 = c->Tcap + 1; a.t = t; a.mode = mode;
+  a.Gb = Gb; a.T1 = c->Tcap + 1; a.t = t; a.mode = mode;
   a.early_stop = early_stop;
   // the dense matrix already carries the 1/sqrt(n) of sparc_ldpc.py:143-146
   a.sqrt_n = c->backend == SA_BACKEND_DENSE ? (real)1 : (real)std::sqrt((double)c->n);
@@ -964,13 +1356,58 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G) {
   return a;
 }
 
+// Row splits for small batches: enough workgroups to cover every CU.
+int row_splits(const sa_ctx* c, int B) {
+  const int wgs = c->G * B;
+  int rs = (c->n_cus + wgs - 1) / wgs;
+  return rs < 1 ? 1 : (rs > 4 ? 4 : rs);
+}
+
 template <typename real, int E>
-void launch_sec_e(sa_ctx* c, int B, const SecArgs<real>& a) {
-  dim3 grid(c->G, B);
+void launch_sec_e(sa_ctx* c, int B, SecArgs<real> a) {
+  a.RS = row_splits(c, B);
+  dim3 grid(c->G * a.RS, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
   k_sec<real, E><<<grid, 256, c->sec_lds, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
 }
+
+// Batched section kernel: grid = Gb groups x ceil(B / CB) chunks (1-D, XCD-grouped).
+template <typename real, int E, int CB>
+void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
+  a.G = c->Gb;
+  a.B = B;
+  a.NC = (B + CB - 1) / CB;
+  if (c->prof) c->prof->begin(c->stream, K_SEC);
+  k_secb<real, E, CB, kWB><<<c->Gb * a.NC, kWB * 64, c->secb_lds, c->stream>>>(a);
+  if (c->prof) c->prof->end(c->stream);
+}
+
+template <typename real, int CB>
+int launch_secb_cb(sa_ctx* c, int B, const SecArgs<real>& a) {
+  switch (c->E) {
+    case 1: launch_secb_e<real, 1, CB>(c, B, a); break;
+    case 2: launch_secb_e<real, 2, CB>(c, B, a); break;
+    case 4: launch_secb_e<real, 4, CB>(c, B, a); break;
+    case 8: launch_secb_e<real, 8, CB>(c, B, a); break;
+    case 16: launch_secb_e<real, 16, CB>(c, B, a); break;
+    default: return fail(SA_ERR_UNSUPPORTED, "batched kernel: M > 1024");
+  }
+  return SA_OK;
+}
+
+template <typename real>
+int launch_secb(sa_ctx* c, int B, int t, int es) {
+  SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
+  int rc;
+  if (c->CB == 2) rc = launch_secb_cb<real, 2>(c, B, a);
+  else rc = launch_secb_cb<real, 1>(c, B, a);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
+bool use_batched(const sa_ctx* c, int B) { return c->CB > 0 && B >= 4; }
 
 template <typename real>
 int launch_sec(sa_ctx* c, int B, int mode, int t, int es) {
@@ -990,8 +1427,8 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es) {
 }
 
 template <typename real>
-int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G) {
-  RowArgs<real> a = row_args<real>(c, mode, t, es, G);
+int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb) {
+  RowArgs<real> a = row_args<real>(c, mode, t, es, G, Gb);
   dim3 grid(c->NZ, B);
   if (c->prof) c->prof->begin(c->stream, K_ROW);
   k_row<real><<<grid, kRowWaves * 64, 0, c->stream>>>(a);
@@ -1063,10 +1500,10 @@ int seq_ab(sa_ctx* c, int B) {
   int rc;
   if (c->backend == SA_BACKEND_DENSE) {
     if ((rc = launch_dense_ab(c, B, 0, 0, 1))) return rc;
-    return launch_row<real>(c, B, ROW_ABOUT, 0, 0, c->KS);
+    return launch_row<real>(c, B, ROW_ABOUT, 0, 0, c->KS, c->Gd);
   }
   if ((rc = launch_sec<real>(c, B, SEC_AB, 0, 0))) return rc;
-  return launch_row<real>(c, B, ROW_ABOUT, 0, 0, c->G);
+  return launch_row<real>(c, B, ROW_ABOUT, 0, 0, c->G, c->G);
 }
 
 // Az of the batch staged in d_z -> d_out  (B x L*M)
@@ -1095,27 +1532,35 @@ template <typename real>
 int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const int es = (flags & SA_FLAG_NO_EARLY_STOP) ? 0 : 1;
   const bool dense = c->backend == SA_BACKEND_DENSE;
-  const int G = dense ? c->KS : c->G;
+  const bool batched = !dense && use_batched(c, B);
+  // partial counts of the producer of abp (Ab) and bbp (beta^2)
+  const int G = dense ? c->KS : (batched ? c->Gb : c->G);
+  const int Gb = dense ? c->Gd : (batched ? c->Gb : c->G);
   int rc;
   HIP_TRY(hipMemsetAsync(c->d_iters, 0xff, (size_t)B * sizeof(int), c->stream));
   if (has_b0) {
-    if (dense) rc = launch_dense_ab(c, B, 0, 0, 1);
-    else rc = launch_sec<real>(c, B, SEC_AB, 0, 0);
-    if (rc) return rc;
-    if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, G))) return rc;
+    if (dense) {
+      if ((rc = launch_dense_ab(c, B, 0, 0, 1))) return rc;
+      if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, c->KS, c->Gd))) return rc;
+    } else {
+      if ((rc = launch_sec<real>(c, B, SEC_AB, 0, 0))) return rc;
+      if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, c->G, c->G))) return rc;
+    }
   } else {
     HIP_TRY(hipMemsetAsync(c->d_beta, 0, (size_t)B * c->L * c->M * rsz(c), c->stream));
-    if ((rc = launch_row<real>(c, B, ROW_INIT0, 0, 0, G))) return rc;
+    if ((rc = launch_row<real>(c, B, ROW_INIT0, 0, 0, G, Gb))) return rc;
   }
   for (int t = 0; t < T; ++t) {
     if (dense) {
       if ((rc = launch_dense_az(c, B, t, es, 0))) return rc;
       if ((rc = launch_dense_den(c, B, t, es))) return rc;
       if ((rc = launch_dense_ab(c, B, t, es, 0))) return rc;
+    } else if (batched) {
+      if ((rc = launch_secb<real>(c, B, t, es))) return rc;
     } else {
       if ((rc = launch_sec<real>(c, B, SEC_AMP, t, es))) return rc;
     }
-    if ((rc = launch_row<real>(c, B, ROW_AMP, t, es, G))) return rc;
+    if ((rc = launch_row<real>(c, B, ROW_AMP, t, es, G, Gb))) return rc;
   }
   k_iters_final<<<(B + 255) / 256, 256, 0, c->stream>>>(c->d_iters, B, T);
   HIP_TRY(hipGetLastError());
@@ -1177,7 +1622,7 @@ int build_tables(sa_ctx* c) {
   const int L = c->L, n = c->n, w = c->w, M = c->M;
   const int lgM = ilog2(M);
   std::vector<uint16_t> inv((size_t)L * w, (uint16_t)n);
-  const int G = (L + kSpw - 1) / kSpw;
+  const int G = (L + kSG - 1) / kSG * (kSG / kSpw);  // padded to whole batched groups
   std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);  // [G][n][4]; missing sections -> (k 0, +)
   for (int l = 0; l < L; ++l) {
     const uint32_t* o = c->ordering.data() + (size_t)l * n;
@@ -1220,6 +1665,32 @@ int build_dense(sa_ctx* c) {
   return SA_OK;
 }
 
+// Allow every section-kernel instantiation the full 160 KB LDS (once per process).
+template <typename real>
+hipError_t lds_attr_all() {
+  const int mx = 160 * 1024;
+  hipError_t e = hipSuccess;
+#define SA_A(F) if (e == hipSuccess) e = hipFuncSetAttribute((const void*)F, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+  SA_A((k_sec<real, 1>)) SA_A((k_sec<real, 2>)) SA_A((k_sec<real, 4>)) SA_A((k_sec<real, 8>))
+  SA_A((k_sec<real, 16>)) SA_A((k_sec<real, 32>)) SA_A((k_sec<real, 64>))
+  SA_A((k_secb<real, 1, 1, kWB>)) SA_A((k_secb<real, 2, 1, kWB>)) SA_A((k_secb<real, 4, 1, kWB>))
+  SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
+  SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
+  SA_A((k_secb<real, 8, 2, kWB>)) SA_A((k_secb<real, 16, 2, kWB>))
+#undef SA_A
+  return e;
+}
+
+int set_lds_limits() {
+  static int done = 0;
+  if (done) return SA_OK;
+  hipError_t e = lds_attr_all<float>();
+  if (e == hipSuccess) e = lds_attr_all<double>();
+  if (e != hipSuccess) return fail(SA_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+  done = 1;
+  return SA_OK;
+}
+
 int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int backend, int prec,
                 int device) {
   if (!out) return fail(SA_ERR_ARG, "out is NULL");
@@ -1254,6 +1725,22 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     return fail(SA_ERR_UNSUPPORTED, "section kernel does not fit in LDS (n and M too large for this precision)");
   }
   c->G = (L + kSpw - 1) / kSpw;
+  c->Gb = (L + kWB - 1) / kWB;
+  // batched kernel: CB = 2 when two workgroups still fit a CU's LDS, else 1
+  for (int cb = 2; cb >= 1 && M <= 1024; --cb) {
+    const size_t zb = (((size_t)(n + 1) * cb * s) + 15) / 16 * 16;
+    const size_t need = zb + (size_t)kWB * M * cb * s + (size_t)kWB * cb * s;
+    if (need <= (cb == 1 ? 160 : 80) * 1024) {
+      c->CB = cb;
+      c->secb_lds = need;
+      break;
+    }
+  }
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      c->n_cus = prop.multiProcessorCount;
+  }
   c->Gd = (L + 3) / 4;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -1274,22 +1761,9 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     sa_destroy(c);
     return rc;
   }
-  if (c->sec_lds > 64 * 1024) {
-    hipError_t e = hipSuccess;
-    switch (c->E) {
-#define SA_ATTR(EE)                                                                                    \
-  case EE:                                                                                             \
-    e = prec == SA_PREC_F64                                                                            \
-            ? hipFuncSetAttribute((const void*)k_sec<double, EE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->sec_lds) \
-            : hipFuncSetAttribute((const void*)k_sec<float, EE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->sec_lds);  \
-    break;
-      SA_ATTR(1) SA_ATTR(2) SA_ATTR(4) SA_ATTR(8) SA_ATTR(16) SA_ATTR(32) SA_ATTR(64)
-#undef SA_ATTR
-    }
-    if (e != hipSuccess) {
-      sa_destroy(c);
-      return fail(SA_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-    }
+  if ((rc = set_lds_limits())) {
+    sa_destroy(c);
+    return rc;
   }
   *out = c;
   return SA_OK;
@@ -1538,5 +2012,13 @@ int sa_device_count(void) {
 const char* sa_last_error(void) { return g_err.c_str(); }
 
 const char* sa_version(void) { return SA_VERSION; }
+
+#ifdef SA_STAMPS
+int sa_debug_stamps(unsigned long long* out) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
+  return SA_OK;
+}
+#endif
 
 }  // extern "C"

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""BER-vs-Eb/N0 sweeps on the MI355X next to the reference's published curves.
+
+  plain   : waterfall()'s BER_plain column (sparc_ldpc.py:1126-1282):
+            L=M=512 P=4 R=5/6 T=64, Eb/N0 = linspace(3, 10, 10) dB (20*log10),
+            MIN_ERRORS=200 / MAX_BLOCKS=250.
+  l768    : soft_hard_plot()'s BER_sparc column (sparc_ldpc.py:1285-1432):
+            L=768 M=512 P=1.8 at the overall rate R=0.8765 (sec=569),
+            sigma = linspace(0.8, 0.4, 10), 100 reps per point.
+
+One process per GPU (torchrun); reps sharded by rank, per-round counters
+summed over RCCL.  Writes <out>.csv (reference schema) and <out>.json.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sweep", default="plain", choices=["plain", "l768"])
+    ap.add_argument("--points", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--out", default="gpurun_out/waterfall")
+    ap.add_argument("--precision", default="fp32")
+    args = ap.parse_args()
+    import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd import dist
+    rank, world, _ = dist.init()
+    with open(os.path.join(ROOT, "tests", "golden", "published_ber.json")) as fh:
+        pub = json.load(fh)
+    t0 = time.time()
+    if args.sweep == "plain":
+        cfg = pub["waterfall_plain"]["config"]
+        ebno = np.linspace(3, 10, 10)[:args.points]
+        rows = sp.waterfall_plain(cfg["L"], cfg["M"], cfg["P"], cfg["R"], cfg["T"], ebno,
+                                  cfg["MIN_ERRORS"], cfg["MAX_BLOCKS"],
+                                  csv_filename=args.out + ".csv" if rank == 0 else None,
+                                  batch=args.batch, precision=args.precision, rank=rank, world=world,
+                                  allreduce=dist.allreduce_sum)
+        ref = pub["waterfall_plain"]["BER_plain_runs"]
+        for i, r in enumerate(rows):
+            r["reference_runs"] = [v[i] for v in ref.values()]
+    else:
+        cfg = pub["soft_hard_BER_sparc"]["config"]
+        L, M, P, T = cfg["L"], cfg["M"], cfg["P"], cfg["T"]
+        logm = np.log2(M)
+        n_coded = L * logm / 1
+        R = (L * logm - 9 * 569 * (1 - 5 / 6)) / n_coded
+        n = int(L * logm / R)
+        op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=args.precision)
+        Pl = P / L * np.ones(L)
+        rows = []
+        for i, sigma in enumerate(np.linspace(0.8, 0.4, 10)[:args.points]):
+            reps = cfg["reps_per_point"]
+            seeds = [j for j in range(i * 100000, i * 100000 + reps) if j % world == rank]
+            be, it = sp.mc_decode(op, Pl, sigma, T, seeds, batch=args.batch)
+            tot = dist.allreduce_sum(np.array([be.sum(), len(seeds), it.sum()], dtype=np.int64))
+            ebno_db = 20 * np.log10(1 / (2 * R) * (P / sigma ** 2))  # sparc_ldpc.py:1414-1416
+            rows.append(dict(EbN0_dB=float(ebno_db), BER_sparc=float(tot[0] / (tot[1] * L * logm)),
+                             blocks=int(tot[1]), mean_iters=float(tot[2] / tot[1]),
+                             reference=pub["soft_hard_BER_sparc"]["BER_sparc"][i]))
+    if rank == 0:
+        res = dict(sweep=args.sweep, world=world, seconds=time.time() - t0, rows=rows)
+        with open(args.out + ".json", "w") as fh:
+            json.dump(res, fh, indent=1)
+        for r in rows:
+            print(json.dumps(r))
+        print(f"# {args.sweep}: {time.time() - t0:.1f} s on {world} GPU(s)")
+    dist.finalize()
+
+
+if __name__ == "__main__":
+    main()

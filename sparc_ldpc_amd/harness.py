@@ -24,7 +24,7 @@ from .operators import SparcOperator, make_ordering, sparc_transforms, sparc_tra
 
 __all__ = [
     "SPARCParams", "LDPCParams", "pa_parameterised", "bits2indices", "ber_of",
-    "amp_ldpc_sim", "mc_decode", "ebno_to_sigma", "waterfall_plain", "amp_test_reps",
+    "amp_ldpc_sim", "mc_decode", "ebno_to_sigma", "ber_point", "waterfall_plain", "amp_test_reps",
 ]
 
 
@@ -126,17 +126,17 @@ def mc_decode(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True
     """Batched Monte-Carlo reps on one device (SURVEY §8d synthetic inputs).
 
     Rep with seed s: ``RandomState(s)`` draws the L section indices uniform
-    in [0, M) (same law as random bits -> bits2indices) and then the noise
-    N(0, σ²) (n values).  Encoding x = A β₀ runs on the device (batched Ab).
-    Returns dict of int64 counters: bit_errors, blocks, block_errors, iters,
-    section_errors.
+    in [0, M) (the same law as random bits -> bits2indices) and then the
+    noise N(0, σ²) (n values).  Encoding x = A β₀, decoding and the section
+    decisions run on the device.  Returns per-rep int64 arrays
+    (bit_errors, iters) in seed order.
     """
     L, M, n = op.L, op.M, op.n
-    logm = int(np.log2(M))
     Pl = np.asarray(Pl, dtype=np.float64)
     c = np.sqrt(n * Pl)
-    acc = dict(bit_errors=0, blocks=0, block_errors=0, iters=0, section_errors=0)
     seeds = list(seeds)
+    bit_errors = np.zeros(len(seeds), dtype=np.int64)
+    iters = np.zeros(len(seeds), dtype=np.int64)
     for s0 in range(0, len(seeds), batch):
         chunk = seeds[s0:s0 + batch]
         B = len(chunk)
@@ -149,16 +149,11 @@ def mc_decode(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True
         beta0 = np.zeros((B, L * M))
         beta0[np.arange(B)[:, None], np.arange(L)[None, :] * M + idx] = c[None, :]
         y = op.Ab_batch(beta0) + noise
-        _, iters = op.amp_batch(y, Pl, T, None, early_stop)
+        _, it = op.amp_batch(y, Pl, T, None, early_stop)
         rx = op.decide(B).astype(np.int64)
-        be = _popcount(np.bitwise_xor(idx, rx)).sum(axis=1)
-        acc["bit_errors"] += int(be.sum())
-        acc["blocks"] += B
-        acc["block_errors"] += int((be > 0).sum())
-        acc["iters"] += int(iters.sum())
-        acc["section_errors"] += int((idx != rx).sum())
-    acc["total_bits_per_block"] = L * logm
-    return acc
+        bit_errors[s0:s0 + B] = _popcount(np.bitwise_xor(idx, rx)).sum(axis=1)
+        iters[s0:s0 + B] = it
+    return bit_errors, iters
 
 
 def ebno_to_sigma(ebno_db, P, R):
@@ -168,40 +163,80 @@ def ebno_to_sigma(ebno_db, P, R):
     return float(np.sqrt(P / snr))
 
 
+def ber_point(decode_round, total_bits, min_errors, max_blocks, batch, rank=0, world=1,
+              allreduce=None, seed_base=0):
+    """One Eb/N0 point with the reference's stopping rule (sparc_ldpc.py:1217-1245):
+
+        while nblockerrors < MIN_ERRORS:
+            decode one block; ber_cum += ber; nblockerrors += (ber > 0); nblocks += 1
+            if nblocks >= MAX_BLOCKS: break
+        BER = ber_cum / nblocks
+
+    Blocks are decoded in rounds of batch*world (rank r takes the seeds of
+    ``dist.shard_seeds``); each round's per-block bit errors are summed over
+    ranks into global seed order (an all-gather by sum, batch*world int64)
+    and consumed block by block, so the result equals a sequential run over
+    the same seeds whatever the world size.  ``decode_round(seeds)`` returns
+    the per-block (bit_errors, iters) of this rank's seeds.
+    """
+    from .dist import shard_seeds
+    ber_cum = 0.0
+    nerr = nblocks = iters = errbits = 0
+    rnd = 0
+    while nerr < min_errors:
+        seeds = shard_seeds(seed_base, rnd, batch, rank, world)
+        be, it = decode_round(seeds)
+        glob = np.zeros((2, batch * world), dtype=np.int64)
+        glob[0, rank::world] = be   # global position of seed base + rnd*B*W + j is j
+        glob[1, rank::world] = it
+        if allreduce is not None:
+            glob = allreduce(glob)
+        done = False
+        for j in range(batch * world):
+            if nerr >= min_errors:
+                done = True
+                break
+            b = int(glob[0, j])
+            ber_cum += b / total_bits
+            errbits += b
+            iters += int(glob[1, j])
+            nerr += 1 if b > 0 else 0
+            nblocks += 1
+            if nblocks >= max_blocks:
+                done = True
+                break
+        if done:
+            break
+        rnd += 1
+    return dict(BER=ber_cum / nblocks, blocks=nblocks, block_errors=nerr, bit_errors=errbits,
+                mean_iters=iters / nblocks)
+
+
 def waterfall_plain(L, M, P, R, T, ebno_dbs, min_errors=200, max_blocks=250, csv_filename=None,
                     batch=64, seed0=0, backend=None, precision=None, rank=0, world=1, allreduce=None):
-    """BER_plain column of waterfall() (sparc_ldpc.py:1126-1282) on the GPU.
-
-    Stopping rule per Eb/N0 point as the reference: keep drawing blocks until
-    ``min_errors`` blocks with errors or ``max_blocks`` blocks (:1217-1245);
-    BER = mean per-block BER (= Σ bit errors / (blocks · bits)).  Reps are
-    sharded over ``world`` ranks (rank r takes seeds ≡ r mod world) and the
-    int64 counters are summed with ``allreduce`` (RCCL via torch.distributed
-    in the multi-GPU harness) once per round of batch·world reps.
-    Writes the reference CSV schema (:1257-1264) when csv_filename is given.
+    """BER_plain column of waterfall() (sparc_ldpc.py:1126-1282) on the GPU:
+    plain SPARC at rate R, 20*log10 Eb/N0 -> sigma mapping, the reference's
+    MIN_ERRORS / MAX_BLOCKS rule (``ber_point``), reps sharded over ranks.
+    Writes the reference CSV schema (:1257-1264) when csv_filename is given
+    (only the BER_plain column is produced; the LDPC columns are 0).
     """
     n = int(L * np.log2(M) / R)
     ordering = make_ordering(L, M, n, 0)
     op = SparcOperator(L, M, n, ordering, backend, precision)
     Pl = P / L * np.ones(L)
+    total_bits = int(L * np.log2(M))
     rows = []
     for pi, ebno_db in enumerate(ebno_dbs):
         sigma = ebno_to_sigma(ebno_db, P, R)
-        tot = np.zeros(4, dtype=np.int64)  # bit_errors, blocks, block_errors, iters
-        rnd = 0
-        while tot[2] < min_errors and tot[1] < max_blocks:
-            base = seed0 + pi * 10_000_000 + rnd * batch * world
-            seeds = [base + rank + world * i for i in range(batch)]
-            r = mc_decode(op, Pl, sigma, T, seeds, batch=batch)
-            part = np.array([r["bit_errors"], r["blocks"], r["block_errors"], r["iters"]], dtype=np.int64)
-            if allreduce is not None:
-                part = allreduce(part)
-            tot += part
-            rnd += 1
-        ber = tot[0] / (tot[1] * L * np.log2(M))
-        rows.append(dict(EbN0_dB=ebno_db, BER_amp_1=0.0, BER_ldpc=0.0, BER_amp_2=0.0,
-                         BER_ldpc_2=0.0, BER_plain=ber, BER_bpsk=0.0,
-                         blocks=int(tot[1]), block_errors=int(tot[2]), mean_iters=tot[3] / tot[1]))
+
+        def round_fn(seeds, sigma=sigma):
+            return mc_decode(op, Pl, sigma, T, seeds, batch=batch)
+
+        r = ber_point(round_fn, total_bits, min_errors, max_blocks, batch, rank, world, allreduce,
+                      seed_base=seed0 + pi * 10_000_000)
+        rows.append(dict(EbN0_dB=float(ebno_db), BER_amp_1=0.0, BER_ldpc=0.0, BER_amp_2=0.0,
+                         BER_ldpc_2=0.0, BER_plain=r["BER"], BER_bpsk=0.0, blocks=r["blocks"],
+                         block_errors=r["block_errors"], mean_iters=r["mean_iters"]))
     if csv_filename and rank == 0:
         fields = ['EbN0_dB', 'BER_amp_1', 'BER_ldpc', 'BER_amp_2', 'BER_ldpc_2', 'BER_plain', 'BER_bpsk']
         with open(csv_filename, 'a', newline='') as fh:

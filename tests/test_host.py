@@ -1,0 +1,192 @@
+"""CPU: the C-ABI library's export table, the host-side mirror of the
+reference interface, and the multi-rank Monte-Carlo logic (gloo)."""
+import hashlib
+import json
+import os
+import re
+import socket
+import ctypes as ct
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, golden
+from oracle import amp_oracle as orc
+
+
+# ---- C ABI --------------------------------------------------------------
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "sparc_amp.h")) as fh:
+        txt = fh.read()
+    return sorted(set(re.findall(r"\b(sa_[a-z0-9_A-Z]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from sparc_ldpc_amd import _lib
+    lib = ct.CDLL(_lib.LIB_PATH)
+    syms = _header_symbols()
+    assert syms, "no declarations parsed"
+    for name in syms:
+        assert hasattr(lib, name), f"{name} declared in include/sparc_amp.h but not exported"
+    assert sorted(_lib.EXPORTS) == syms
+
+
+def test_library_loads_without_gpu_and_fails_loudly():
+    import sparc_ldpc_amd as sp
+    lib = sp.load_library()
+    assert lib.sa_version().startswith(b"sparc_amp")
+    if lib.sa_device_count() == 0:
+        ctx = ct.c_void_p()
+        o = np.ones((2, 8), dtype=np.uint32)
+        rc = lib.sa_create(ct.byref(ctx), 2, 4, 8, o.ctypes.data_as(ct.POINTER(ct.c_uint32)), 0, 0, 0)
+        assert rc == -6  # SA_ERR_NO_DEVICE: no silent CPU fallback
+        assert b"device" in lib.sa_last_error()
+        with pytest.raises(sp.SparcAmpError):
+            sp.SparcOperator(2, 4, 8, o)
+
+
+def test_null_context_is_an_argument_error():
+    import sparc_ldpc_amd as sp
+    lib = sp.load_library()
+    assert lib.sa_Ab(None, 1, None, None) == -1
+    assert lib.sa_run(None, 1, 1, 0) == -1
+    lib.sa_destroy(None)  # no-op
+
+
+# ---- host mirror of the reference interface ------------------------------
+
+def test_make_ordering_matches_reference_hashes():
+    import sparc_ldpc_amd as sp
+    with open(os.path.join(GOLDEN, "meta.json")) as fh:
+        meta = json.load(fh)
+    for key, h in meta["ordering_sha256"].items():
+        L, M, n = (int(p[1:]) for p in key.split("_"))
+        o = sp.make_ordering(L, M, n, 0)
+        assert hashlib.sha256(o.tobytes()).hexdigest() == h
+        assert o is sp.make_ordering(L, M, n, 0)  # memoised like the reference's seed-0 reuse
+
+
+def test_bits_indices_ber_against_oracle():
+    import sparc_ldpc_amd as sp
+    rs = np.random.RandomState(4)
+    for M in (2, 4, 512):
+        logm = int(np.log2(M))
+        bits = rs.randint(0, 2, 37 * logm).tolist()
+        assert sp.bits2indices(bits, M) == orc.bits2indices(bits, M)
+        a = rs.randint(0, M, 37)
+        b = rs.randint(0, M, 37)
+        assert sp.ber_of(a, b, 37 * logm) == orc.ber_indices(a, b, 37 * logm)
+
+
+def test_ebno_mapping_matches_reference_fixture():
+    import sparc_ldpc_amd as sp
+    g = golden("c5_reps.npz")
+    assert sp.ebno_to_sigma(float(g["ebno_db"]), float(g["P"]), float(g["R"])) == float(g["sigma"])
+
+
+def test_pa_parameterised_matches_oracle():
+    import sparc_ldpc_amd as sp
+    a = sp.pa_parameterised(64, 1.3, 4.0, 0.8, 0.7)
+    b = orc.pa_parameterised(64, 1.3, 4.0, 0.8, 0.7)
+    assert np.array_equal(a, b) and abs(a.sum() - 4.0) < 1e-12
+
+
+def test_beta0_sentinels():
+    from sparc_ldpc_amd.amp import _beta0
+    assert _beta0(None, 2, 4) is None
+    assert _beta0(np.array([None]), 2, 4) is None  # the reference's default (sparc_ldpc.py:189)
+    z = _beta0(np.zeros((8, 1)), 2, 4)
+    assert z.shape == (1, 8) and not z.any()
+    with pytest.raises(AssertionError):
+        _beta0(np.zeros(7), 2, 4)
+
+
+def test_amp_rejects_foreign_operators():
+    import sparc_ldpc_amd as sp
+    with pytest.raises(TypeError):
+        sp.amp(np.zeros(8), 0, np.ones(2), 2, 4, 3, lambda b: b, lambda z: z)
+
+
+# ---- Monte-Carlo stopping rule and sharding --------------------------------
+
+def _fake_round(seeds):
+    """Deterministic stand-in for mc_decode: bit errors as a function of the seed."""
+    s = np.asarray(seeds, dtype=np.int64)
+    be = np.where(s % 3 == 0, (s * 7) % 11, 0).astype(np.int64)
+    return be, (s % 5 + 10).astype(np.int64)
+
+
+def _reference_loop(seed_base, total_bits, min_errors, max_blocks):
+    """sparc_ldpc.py:1217-1245 written out block by block."""
+    ber_cum = 0.0
+    nerr = nblocks = 0
+    s = seed_base
+    while nerr < min_errors:
+        be, _ = _fake_round([s])
+        ber = be[0] / total_bits
+        ber_cum += ber
+        if ber:
+            nerr += 1
+        nblocks += 1
+        s += 1
+        if nblocks >= max_blocks:
+            break
+    return ber_cum / nblocks, nblocks, nerr
+
+
+@pytest.mark.parametrize("min_errors,max_blocks,batch", [(5, 250, 8), (200, 37, 16), (3, 1000, 1)])
+def test_ber_point_matches_sequential_reference_rule(min_errors, max_blocks, batch):
+    import sparc_ldpc_amd as sp
+    r = sp.ber_point(_fake_round, 4608, min_errors, max_blocks, batch, seed_base=100)
+    ber, nb, ne = _reference_loop(100, 4608, min_errors, max_blocks)
+    assert r["blocks"] == nb and r["block_errors"] == ne
+    assert abs(r["BER"] - ber) <= 1e-15
+
+
+def test_shard_seeds_partition():
+    from sparc_ldpc_amd.dist import shard_seeds
+    for world in (1, 2, 8):
+        allseeds = []
+        for rnd in range(3):
+            for rank in range(world):
+                allseeds += shard_seeds(50, rnd, 4, rank, world)
+        assert sorted(allseeds) == list(range(50, 50 + 3 * 4 * world))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gloo_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd import dist
+    dist.init("gloo")
+    res = sp.ber_point(_fake_round, 4608, 7, 250, 4, rank, world, dist.allreduce_sum, seed_base=100)
+    c = dist.allreduce_sum(np.array([rank + 1], dtype=np.int64))
+    out.put((rank, res, int(c[0])))
+    dist.finalize()
+
+
+def test_ber_point_two_ranks_gloo_equals_single():
+    import multiprocessing as mp
+    import sparc_ldpc_amd as sp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = sp.ber_point(_fake_round, 4608, 7, 250, 8, seed_base=100)
+    for rank, res, csum in got:
+        assert csum == 3  # the counter all-reduce itself
+        assert res["blocks"] == single["blocks"] and res["block_errors"] == single["block_errors"]
+        assert abs(res["BER"] - single["BER"]) <= 1e-15

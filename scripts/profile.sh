@@ -1,15 +1,27 @@
 #!/bin/bash
-# rocprofv3 kernel-trace summaries for the bench workloads (run on the GPU box).
+# rocprofv3 summaries for a bench workload (run on the GPU box):
+#   pass 1: --kernel-trace --stats        -> per-kernel durations
+#   pass 2: --pmc FETCH_SIZE (own pass)   -> HBM read bytes per dispatch
+#   pass 3: --pmc WRITE_SIZE (own pass)   -> HBM write bytes per dispatch
 # Usage: bash scripts/profile.sh TAG [bench args...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-run}; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT -o $TAG --output-format csv -- \
-  python3 bench.py --no-cpu --no-dense "$@" > $OUT/bench.log 2>&1
+run() {  # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 600 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- \
+    python3 bench.py --no-cpu --no-dense "${BENCH_ARGS[@]}" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  return $rc
+}
+BENCH_ARGS=("$@")
+run trace --kernel-trace --stats && \
+run fetch --kernel-trace --pmc FETCH_SIZE && \
+run write --kernel-trace --pmc WRITE_SIZE
 rc=$?
-echo "rocprof rc=$rc"; tail -n 2 $OUT/bench.log | cut -c1-600
-f=$(find $OUT -name "*kernel_stats.csv" | head -1)
+f=$(find $OUT/trace -name "*kernel_stats.csv" | head -1)
 [ -n "$f" ] && cat "$f"
 exit $rc

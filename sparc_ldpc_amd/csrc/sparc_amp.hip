@@ -1726,7 +1726,8 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   }
   c->G = (L + kSpw - 1) / kSpw;
   c->Gb = (L + kWB - 1) / kWB;
-  // batched kernel: CB = 2 when two workgroups still fit a CU's LDS, else 1
+  // batched kernel: CB = 2 codewords per workgroup when two workgroups still
+  // fit a CU's LDS (occupancy beats fewer Ab partials: measured), else 1
   for (int cb = 2; cb >= 1 && M <= 1024; --cb) {
     const size_t zb = (((size_t)(n + 1) * cb * s) + 15) / 16 * 16;
     const size_t need = zb + (size_t)kWB * M * cb * s + (size_t)kWB * cb * s;

@@ -626,13 +626,66 @@ __device__ __forceinline__ void vstore(real* p, const real (&o)[CB]) {
   *reinterpret_cast<V*>(p) = t;
 }
 
+// LDS byte offset of the 16-bit row index in half `HALF` of w, scaled by
+// 2^SH (the [row][CB] element size): one SDWA VALU op (word select + shift).
+template <int SH, int HALF>
+__device__ __forceinline__ unsigned sdwa_shl16(unsigned w) {
+  unsigned r;
+  if constexpr (HALF == 0)
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+        : "=v"(r) : "v"(w), "i"(SH));
+  else
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+        : "=v"(r) : "v"(w), "i"(SH));
+  return r;
+}
+
+template <int N>
+constexpr int ilog2c() { return N <= 1 ? 0 : 1 + ilog2c<N / 2>(); }
+
+// One h-step of the bucket gather for E >= 4 (Q = 4): the wave's 4*NQ
+// bucket rows are turned into LDS addresses, all E gathers are issued, then
+// v[c][i] += sgn(h) * z[row][c] as fmas with a wave-uniform sign.
+template <typename real, int E, int CB>
+__device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ushort4 (&t)[(E + 3) / 4],
+                                             real sg, real (&v)[CB][E]) {
+  constexpr int SH = ilog2c<CB * (int)sizeof(real)>();
+  unsigned ad[E];
+#pragma unroll
+  for (int j = 0; j < E / 4; ++j) {
+    const uint2 w = *reinterpret_cast<const uint2*>(&t[j]);
+    ad[4 * j + 0] = sdwa_shl16<SH, 0>(w.x);
+    ad[4 * j + 1] = sdwa_shl16<SH, 1>(w.x);
+    ad[4 * j + 2] = sdwa_shl16<SH, 0>(w.y);
+    ad[4 * j + 3] = sdwa_shl16<SH, 1>(w.y);
+  }
+  // zsb is the start of the dynamic LDS region, which is LDS address 0 in
+  // this kernel (it declares no static LDS: checked on the host at context
+  // creation), so the scaled row index is the LDS address itself.
+  (void)zsb;
+  using V = real __attribute__((ext_vector_type(CB)));
+  using lds_v = __attribute__((address_space(3))) const V;
+  real zz[E][CB];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const V x = *reinterpret_cast<lds_v*>((size_t)ad[i]);
+#pragma unroll
+    for (int c = 0; c < CB; ++c) zz[i][c] = x[c];
+  }
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) v[c][i] = fma(zz[i][c], sg, v[c][i]);
+}
+
 template <typename real, int E, int CB, int W>
 __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = W * 64;
   constexpr int NQ = (E + 3) / 4;
-  constexpr int KH = E >= 16 ? 2 : 4;   // bucket h-steps whose table loads are in flight together
-  constexpr int KR = 3;                 // rows per thread whose Ab-table loads are in flight together
+  constexpr int KH = (E >= 16 || CB >= 4) ? 2 : 4;  // bucket h-steps with table loads in flight together
+  constexpr int KR = CB >= 4 ? 2 : 3;   // rows per thread whose Ab-table loads are in flight together
+  constexpr bool PB = CB <= 2;          // prefetch the previous beta with the first loads
   constexpr int W4 = W / 4;             // 4-section table groups per workgroup
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int M = a.M, n = a.n;
@@ -665,10 +718,13 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
   const bool have = l < a.L;
   const int lc = have ? l : a.L - 1;
 
-  real* zs = reinterpret_cast<real*>(smem);  // [(n+1)][CB]
+  // z ([n+1][CB], read by the bucket gather) and T ([W][M][CB], read by the
+  // Ab gather) are never live together: they share one LDS region.
+  real* zs = reinterpret_cast<real*>(smem);
+  real* ts = zs;
   const int zslots = (((n + 1) * CB * (int)sizeof(real) + 15) / 16 * 16) / (int)sizeof(real);
-  real* ts = zs + zslots;                    // [W][M][CB]
-  real* bbw = ts + (size_t)W * M * CB;       // [W][CB]
+  const int region = zslots > W * M * CB ? zslots : W * M * CB;
+  real* bbw = zs + region;                   // [W][CB]
 
   // ---- every load independent of z in flight together ---------------------
   // z rows of the CB codewords (first pass of the staging loop)
@@ -683,10 +739,12 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
   const uint16_t* il = a.inv + (size_t)lc * a.w;
   ushort4 tb[KH][NQ];
   load_buckets<E, KH>(il, 0, a.nhi, M, lane, tb);
-  real bprev[CB][E];
+  real bprev[PB ? CB : 1][E];
+  if constexpr (PB) {
 #pragma unroll
-  for (int c = 0; c < CB; ++c)
-    load_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lane, M);
+    for (int c = 0; c < CB; ++c)
+      load_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lane, M);
+  }
   const real cl = a.c[lc];
   const ushort4* fw = a.fwd + (size_t)g * W4 * n;
   ushort4 f[KR][W4];
@@ -751,17 +809,19 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
 #pragma unroll
       for (int hh = 0; hh < KH; ++hh) {
         if (h0 + hh < a.nhi) {
-          const bool neg = __popc(h0 + hh) & 1;  // sgn(h): high index bits of w-M+c all ones
-#pragma unroll
-          for (int i = 0; i < E; i += Q) {
-            const ushort4 r4 = tb[hh][i / Q];
+          // sgn(h): the high index bits of w-M+c are all ones
+          const real sg = (__popc(h0 + hh) & 1) ? (real)-1 : (real)1;
+          if constexpr (E >= 4) {
+            gather_step4<real, E, CB>(reinterpret_cast<const unsigned char*>(zs), tb[hh], sg, v);
+          } else {
+            const ushort4 r4 = tb[hh][0];
             const unsigned short rr4[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
               real zz[CB];
               vload<real, CB>(zs + (size_t)rr4[q] * CB, zz);
 #pragma unroll
-              for (int c = 0; c < CB; ++c) v[c][i + q] += neg ? -zz[c] : zz[c];
+              for (int c = 0; c < CB; ++c) v[c][q] = fma(zz[c], sg, v[c][q]);
             }
           }
         }
@@ -780,7 +840,9 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
   for (int c = 0; c < CB; ++c) {
     fwht_wave<real, E>(v[c], lane, mlanes);
     real* bl = a.beta + (size_t)bc[c] * LM + (size_t)lc * M;
-    bbl[c] = denoise_section<real, E>(v[c], bprev[c], bl, lane, M, cl, tau2[c], a.sqrt_n, have && live[c]);
+    if constexpr (!PB) load_section<real, E>(bl, bprev[0], lane, M);
+    bbl[c] = denoise_section<real, E>(v[c], bprev[PB ? c : 0], bl, lane, M, cl, tau2[c], a.sqrt_n,
+                                      have && live[c]);
     if (have) {
       fwht_wave<real, E>(v[c], lane, mlanes);  // T_l = H_M beta_l
     } else {
@@ -790,6 +852,7 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
     }
   }
   STAMP(4);
+  __syncthreads();  // every wave is done with z before T overwrites it
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const int e = elem_index<E>(lane, i);
@@ -834,14 +897,17 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
       for (int c = 0; c < CB; ++c) acc[c] = 0;
 #pragma unroll
       for (int q = 0; q < W4; ++q) {
-        const unsigned ff[4] = {f[u][q].x, f[u][q].y, f[u][q].z, f[u][q].w};
+        const uint2 w = *reinterpret_cast<const uint2*>(&f[u][q]);
+        const unsigned hw[4] = {w.x, w.x >> 16, w.y, w.y >> 16};
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
+          // entry = k | sign << 15: T element k of section q*4+s4, sign -> +-1.0
+          const unsigned k = __builtin_amdgcn_ubfe(hw[s4], 0, 15);
+          const real sg = (hw[s4] & 0x8000u) ? (real)-1 : (real)1;
           real t[CB];
-          vload<real, CB>(ts + ((size_t)(q * 4 + s4) * M + (ff[s4] & 0x7fffu)) * CB, t);
-          const bool ng = ff[s4] & 0x8000u;
+          vload<real, CB>(ts + ((size_t)(q * 4 + s4) * M + k) * CB, t);
 #pragma unroll
-          for (int c = 0; c < CB; ++c) acc[c] += ng ? -t[c] : t[c];
+          for (int c = 0; c < CB; ++c) acc[c] = fma(t[c], sg, acc[c]);
         }
       }
       if (r < n) {
@@ -882,8 +948,7 @@ struct RowArgs {
 // and the per-block partial sums of z^2 for the next tau.  64 rows per
 // workgroup (lane = row); the 16 waves split the G Ab partials (all of a
 // wave's loads in flight together), combined in wave order through LDS.
-constexpr int kRowWaves = 16;
-template <typename real>
+template <typename real, int kRowWaves>
 __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   __shared__ real red[kRowWaves][kRowsPerBlk];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -901,7 +966,7 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
     const int g0 = wv * gq, g1 = min(a.G, g0 + gq);
     const real* p = a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
     real acc = 0;
-    constexpr int U = 8;
+    constexpr int U = 16;
     for (int gg = g0; gg < g1; gg += U) {
       real t[U];
 #pragma unroll
@@ -1400,6 +1465,14 @@ template <typename real>
 int launch_secb(sa_ctx* c, int B, int t, int es) {
   SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
   int rc;
+  if constexpr (sizeof(real) == 4) {
+    if (c->CB == 4) {
+      rc = launch_secb_cb<real, 4>(c, B, a);
+      if (rc) return rc;
+      HIP_TRY(hipGetLastError());
+      return SA_OK;
+    }
+  }
   if (c->CB == 2) rc = launch_secb_cb<real, 2>(c, B, a);
   else rc = launch_secb_cb<real, 1>(c, B, a);
   if (rc) return rc;
@@ -1431,7 +1504,12 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb) {
   RowArgs<real> a = row_args<real>(c, mode, t, es, G, Gb);
   dim3 grid(c->NZ, B);
   if (c->prof) c->prof->begin(c->stream, K_ROW);
-  k_row<real><<<grid, kRowWaves * 64, 0, c->stream>>>(a);
+  // few blocks (small batch): 16 waves split the partials; many blocks: 4
+  // waves with deeper per-lane load streams
+  if (B * c->NZ < 4 * c->n_cus)
+    k_row<real, 16><<<grid, 16 * 64, 0, c->stream>>>(a);
+  else
+    k_row<real, 4><<<grid, 4 * 64, 0, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -1677,13 +1755,32 @@ hipError_t lds_attr_all() {
   SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
   SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
   SA_A((k_secb<real, 8, 2, kWB>)) SA_A((k_secb<real, 16, 2, kWB>))
+  if constexpr (sizeof(real) == 4) {
+    SA_A((k_secb<real, 1, 4, kWB>)) SA_A((k_secb<real, 2, 4, kWB>)) SA_A((k_secb<real, 4, 4, kWB>))
+    SA_A((k_secb<real, 8, 4, kWB>)) SA_A((k_secb<real, 16, 4, kWB>))
+  }
 #undef SA_A
   return e;
+}
+
+// gather_step4 addresses LDS absolutely: the batched kernel must have no
+// static LDS in front of its dynamic region.
+template <typename real>
+bool secb_no_static_lds() {
+  hipFuncAttributes at;
+  const void* fs[] = {(const void*)k_secb<real, 4, 1, kWB>, (const void*)k_secb<real, 8, 1, kWB>,
+                      (const void*)k_secb<real, 16, 1, kWB>, (const void*)k_secb<real, 8, 2, kWB>,
+                      (const void*)k_secb<real, 16, 2, kWB>};
+  for (const void* f : fs)
+    if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
+  return true;
 }
 
 int set_lds_limits() {
   static int done = 0;
   if (done) return SA_OK;
+  if (!secb_no_static_lds<float>() || !secb_no_static_lds<double>())
+    return fail(SA_ERR_HIP, "k_secb has static LDS: absolute LDS addressing in gather_step4 is invalid");
   hipError_t e = lds_attr_all<float>();
   if (e == hipSuccess) e = lds_attr_all<double>();
   if (e != hipSuccess) return fail(SA_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
@@ -1726,11 +1823,13 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   }
   c->G = (L + kSpw - 1) / kSpw;
   c->Gb = (L + kWB - 1) / kWB;
-  // batched kernel: CB = 2 codewords per workgroup when two workgroups still
-  // fit a CU's LDS (occupancy beats fewer Ab partials: measured), else 1
-  for (int cb = 2; cb >= 1 && M <= 1024; --cb) {
+  // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for
+  // fp32 only) whose LDS image (z and T share one region) still lets two
+  // workgroups share a CU; CB = 1 takes the whole LDS if it must
+  for (int cb = (s == 4 ? 4 : 2); cb >= 1 && M <= 1024; cb >>= 1) {
     const size_t zb = (((size_t)(n + 1) * cb * s) + 15) / 16 * 16;
-    const size_t need = zb + (size_t)kWB * M * cb * s + (size_t)kWB * cb * s;
+    const size_t tb = (size_t)kWB * M * cb * s;
+    const size_t need = (zb > tb ? zb : tb) + (size_t)kWB * cb * s;
     if (need <= (cb == 1 ? 160 : 80) * 1024) {
       c->CB = cb;
       c->secb_lds = need;

@@ -1823,6 +1823,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   }
   c->G = (L + kSpw - 1) / kSpw;
   c->Gb = (L + kWB - 1) / kWB;
+
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for
   // fp32 only) whose LDS image (z and T share one region) still lets two
   // workgroups share a CU; CB = 1 takes the whole LDS if it must

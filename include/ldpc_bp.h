@@ -67,6 +67,12 @@ int lb_decode(lb_ctx* ctx, int B, const double* ch, double* app, int* iters, int
 int lb_decode_device(lb_ctx* ctx, int B, const double* d_ch, double* d_app, int* d_iters, int algo,
                      double corr_factor, int max_iter);
 
+/* Device buffers of the context sized for B words (ch, app: B x Nv doubles;
+ * iters: B ints), for handing LLRs to / from other device code (the SPARC
+ * glue of libsparc_amp.so) without a host round trip.  lb_run / lb_fetch
+ * operate on them. */
+int lb_buffers(lb_ctx* ctx, int B, double** d_ch, double** d_app, int** d_iters);
+
 /* Measurement helpers: stage B words into the context's device buffers, run
  * (asynchronously), wait, fetch; lb_run_event_ms = device time of the last run. */
 int lb_stage(lb_ctx* ctx, int B, const double* ch);

@@ -47,7 +47,8 @@ enum { SA_PREC_F32 = 0, SA_PREC_F64 = 1 };
 /* sa_amp / sa_run flags */
 enum {
   SA_FLAG_NO_EARLY_STOP = 1, /* run exactly T iterations (ignore the tau == last_tau stop) */
-  SA_FLAG_BETA0 = 0x100      /* sa_run: start from the beta0 staged by sa_stage */
+  SA_FLAG_BETA0 = 0x100,     /* sa_run: start from the beta0 staged by sa_stage */
+  SA_PTR_DEVICE = 0x200      /* sa_llr / sa_soft_beta0 / sa_hard_cancel: llr / app are device pointers */
 };
 
 /* Replaces sparc_transforms(L, M, n, seed) / block_sub_fht(n, M, L, ordering)
@@ -109,6 +110,38 @@ int sa_profile(sa_ctx* ctx, int B, int T, int flags, double* out);
  * section, first index on ties) of the last sa_run / sa_amp, computed on
  * device: idx_out is B x L. */
 int sa_decide(sa_ctx* ctx, int B, int32_t* idx_out);
+
+/* ---- SPARC <-> LDPC glue of the joint decoder (sparc_ldpc.py:359-712) ---
+ * Binary64 kernels on the staged batch; llr / app arrays are [B][ns*log2 M]
+ * (the LDPC bits of sections l0 .. l0+ns-1, MSB first) and may be device
+ * pointers shared with libldpc_bp.so (flag SA_PTR_DEVICE). */
+
+/* Encoder (sparc_ldpc.py:436-446): y[b] = A beta(idx[b]) + noise[b] staged as
+ * the decode input, beta(idx) one-hot with c_l = sqrt(n Pl_l) at column
+ * idx[b][l] of section l.  idx: B x L; noise: B x n or NULL.  Needs Pl staged
+ * (sa_stage(ctx, B, NULL, Pl, NULL)). */
+int sa_encode(sa_ctx* ctx, int B, const int32_t* idx, const double* noise);
+
+/* Hard re-initialisation (sparc_ldpc.py:831-838): stage the one-hot beta0
+ * with c_l at idx[b][l] (B x L) for the next sa_run(..., SA_FLAG_BETA0). */
+int sa_stage_onehot(sa_ctx* ctx, int B, const int32_t* idx);
+
+/* sp2bp + LLR (sparc_ldpc.py:470-479, :257-281) of sections [l0, l0+ns) of
+ * the current beta: llr = nan_to_num(log(1-p) - log(p)), p the bitwise
+ * posterior of beta_l / c_l. */
+int sa_llr(sa_ctx* ctx, int B, int l0, int ns, double* llr, int flags);
+
+/* Soft exchange (sparc_ldpc.py:683-698): beta0 := beta with sections
+ * [l0, l0+ns) replaced by c_l * bp2sp(1/(1+exp(app))), staged for the next
+ * sa_run(..., SA_FLAG_BETA0); the staged y is kept. */
+int sa_soft_beta0(sa_ctx* ctx, int B, int l0, int ns, const double* app, int flags);
+
+/* Hard exchange (sparc_ldpc.py:486-524): idx = bits2indices(app < 0) for
+ * sections [l0, l0+ns) (idx_out: B x ns, may be NULL); if dst is given (a
+ * context over the same n, e.g. sa_subset of the kept sections), stages
+ * y - A beta_hard(idx) as dst's input y. */
+int sa_hard_cancel(sa_ctx* ctx, int B, int l0, int ns, const double* app, int flags, sa_ctx* dst,
+                   int32_t* idx_out);
 
 /* Introspection. */
 int sa_info(const sa_ctx* ctx, int64_t* out8); /* L, M, n, w, backend, precision, device, bytes */

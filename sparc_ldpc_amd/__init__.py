@@ -1,4 +1,4 @@
-"""sparc_ldpc_amd — MI355X (gfx950) SPARC AMP decoder.
+"""sparc_ldpc_amd — MI355X (gfx950) SPARC AMP decoder with its LDPC outer code.
 
 Drop-in for the AMP hot path of Spimp/sparc_ldpc (ldpc/sparc_ldpc.py:14-222,
 ldpc/amp_test.py:14-50): the same names, argument order and return shapes,
@@ -13,6 +13,10 @@ from .amp import amp, amp_test, amp_batch, operator_of
 from .harness import (SPARCParams, LDPCParams, pa_parameterised, bits2indices, ber_of,
                       amp_ldpc_sim, mc_decode, ebno_to_sigma, ber_point, waterfall_plain,
                       amp_test_reps)
+from . import ldpc
+from .ldpc import code, LdpcBpError
+from .joint import (JointDecoder, joint_decoder, soft_amp_ldpc_sim, hardinitbeta_amp_ldpc_sim, sim_ldpc,
+                    waterfall, sp2bp, bp2sp, mc_joint)
 from . import dist
 
 __version__ = "0.1.0"

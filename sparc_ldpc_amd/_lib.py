@@ -30,12 +30,14 @@ SA_PREC_F32 = 0
 SA_PREC_F64 = 1
 SA_FLAG_NO_EARLY_STOP = 1
 SA_FLAG_BETA0 = 0x100
+SA_PTR_DEVICE = 0x200
 
 # Every symbol include/sparc_amp.h declares (tests check the export table).
 EXPORTS = (
     "sa_create", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
     "sa_reserve", "sa_stage", "sa_run", "sa_wait", "sa_fetch", "sa_run_event_ms",
     "sa_profile", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
+    "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
 )
 
 _P = ct.c_void_p
@@ -60,6 +62,11 @@ _SIG = {
     "sa_device_count": (_I, []),
     "sa_last_error": (ct.c_char_p, []),
     "sa_version": (ct.c_char_p, []),
+    "sa_encode": (_I, [_P, _I, ct.POINTER(ct.c_int32), _D]),
+    "sa_stage_onehot": (_I, [_P, _I, ct.POINTER(ct.c_int32)]),
+    "sa_llr": (_I, [_P, _I, _I, _I, _P, _I]),
+    "sa_soft_beta0": (_I, [_P, _I, _I, _I, _P, _I]),
+    "sa_hard_cancel": (_I, [_P, _I, _I, _I, _P, _I, _P, ct.POINTER(ct.c_int32)]),
 }
 
 _lib = None

@@ -481,6 +481,17 @@ int lb_decode_device(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d
   return launch(c, B, d_ch, d_app, d_iters, algo, corr_factor, max_iter);
 }
 
+int lb_buffers(lb_ctx* c, int B, double** d_ch, double** d_app, int** d_iters) {
+  if (!c || B <= 0) return fail(LB_ERR_ARG, "bad buffer request");
+  HIP_TRY(hipSetDevice(c->dev));
+  int rc;
+  if ((rc = ensure_io(c, B))) return rc;
+  if (d_ch) *d_ch = c->d_ch;
+  if (d_app) *d_app = c->d_app;
+  if (d_iters) *d_iters = c->d_it;
+  return LB_OK;
+}
+
 int lb_stage(lb_ctx* c, int B, const double* ch) {
   if (!c || B <= 0 || !ch) return fail(LB_ERR_ARG, "bad stage arguments");
   HIP_TRY(hipSetDevice(c->dev));

@@ -25,6 +25,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -1280,6 +1281,7 @@ struct sa_ctx {
   int32_t* d_idx = nullptr;
   double* d_stage = nullptr;
   size_t stage_cap = 0;
+  double* d_cd = nullptr;  // c_l = sqrt(n Pl_l) in binary64 (joint-decoding glue)
   double P = 0;
   bool power_set = false;
   size_t bytes = 0;
@@ -1692,6 +1694,8 @@ int set_power(sa_ctx* c, const double* Pl) {
   c->P = P;
   int rc = upload(c, c->d_c, cl.data(), c->L);
   if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_cd, cl.data(), (size_t)c->L * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));  // cl is a host temporary
   c->power_set = true;
   return SA_OK;
 }
@@ -1858,6 +1862,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     rc = build_tables(c);
   }
   if (!rc) rc = dev_alloc(c, &c->d_c, (size_t)L * s);
+  if (!rc) rc = dev_alloc(c, (void**)&c->d_cd, (size_t)L * 8);
   if (rc) {
     sa_destroy(c);
     return rc;
@@ -1882,6 +1887,184 @@ __global__ void k_dense_az_reduce(const float* azp, float* out, int RS, size_t l
     out[i] = s;
   }
 }
+
+
+// ---------------------------------------------------------------------------
+// SPARC <-> LDPC glue of the joint decoder (sparc_ldpc.py:257-314, 359-712)
+// ---------------------------------------------------------------------------
+// All of it runs on the device in binary64 on the B codewords of the batch;
+// the LLR / app arrays are handed to and from the LDPC decoder
+// (libldpc_bp.so) as device pointers, so a joint round never leaves HBM.
+namespace {
+
+// Columns of one-hot beta summed per row: for row r of codeword b,
+//   acc = sum_{l in [l0, l0+ns)} c_l * sgn(o_lr) * H_M[k_lr, idx[b][l-l0]]
+// (A[r, l*M + i] = sgn(o_lr) (-1)^popcount(k_lr & i) / sqrt(n), the same
+// factorisation as the section kernels).  out = base - acc/sqrt(n) (hard
+// cancellation, sparc_ldpc.py:508-518) or acc/sqrt(n) + add (encoding,
+// sparc_ldpc.py:436-446).  One thread per row, idx staged in LDS.
+template <typename real>
+__global__ void __launch_bounds__(256) k_colsum(const ushort4* __restrict__ fwd, const double* __restrict__ cd,
+                                                const int32_t* __restrict__ idx, int ldi, int l0, int ns,
+                                                const real* __restrict__ base, const double* __restrict__ add,
+                                                real* __restrict__ out, int n, double sqrt_n) {
+  extern __shared__ int32_t sidx[];
+  const int b = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
+  for (int i = threadIdx.x; i < ns; i += 256) sidx[i] = idx[(size_t)b * ldi + i];
+  __syncthreads();
+  if (r >= n) return;
+  double acc = 0.0;
+  const int g0 = l0 / kSpw, g1 = (l0 + ns + kSpw - 1) / kSpw;
+  for (int g = g0; g < g1; ++g) {
+    const ushort4 f = fwd[(size_t)g * n + r];
+    const unsigned short fq[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int l = g * kSpw + q;
+      if (l < l0 || l >= l0 + ns) continue;
+      const unsigned k = fq[q] & 0x7fffu;
+      const unsigned neg = (fq[q] >> 15) ^ (__popc(k & (unsigned)sidx[l - l0]) & 1u);
+      acc += neg ? -cd[l] : cd[l];
+    }
+  }
+  const double x = acc / sqrt_n;
+  const size_t o = (size_t)b * n + r;
+  out[o] = base ? (real)((double)base[o] - x) : (real)(x + (add ? add[o] : 0.0));
+}
+
+// sp2bp + LLR (sparc_ldpc.py:470-479 -> :257-281): thread per (codeword,
+// section, bit).  p = sum over the entries j of the section whose bit
+// (logM-1-t) is set, ascending j, of beta_j / c_l (the reference's order);
+// llr = nan_to_num(log(1 - p) - log(p)).
+template <typename real>
+__global__ void k_llr(const real* __restrict__ beta, const double* __restrict__ cd, int L, int M, int lgM,
+                      int l0, int ns, int B, double* __restrict__ llr) {
+  const size_t tot = (size_t)B * ns * lgM;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+    const int t = (int)(i % lgM);
+    const size_t bl = i / lgM;
+    const int lp = (int)(bl % ns), b = (int)(bl / ns), l = l0 + lp;
+    const int step = 1 << (lgM - 1 - t);
+    const real* bs = beta + ((size_t)b * L + l) * M;
+    const double c = cd[l];
+    double p = 0.0;
+    for (int k = step; k < M; k += 2 * step)
+      for (int j = k; j < k + step; ++j) p += (double)bs[j] / c;
+    double v = log(1.0 - p) - log(p);
+    if (v != v) v = 0.0;                                 // nan_to_num: NaN -> 0
+    else if (isinf(v)) v = v > 0 ? DBL_MAX : -DBL_MAX;  // +-inf -> +-max
+    llr[i] = v;
+  }
+}
+
+// bp2sp of the LDPC a-posteriori LLRs (sparc_ldpc.py:683-696 -> :283-314):
+// bp_t = 1/(1+exp(app_t)); sp_m = prod_t (bit_t(m) ? bp_t : 1 - bp_t), MSB
+// first.  Thread per (codeword, LDPC section, entry); unnormalised into sp.
+__global__ void k_bp2sp(const double* __restrict__ app, int M, int lgM, int ns, int B, double* __restrict__ sp) {
+  const size_t tot = (size_t)B * ns * M;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i % M);
+    const size_t bl = i / M;  // b * ns + lp
+    const double* a = app + bl * lgM;
+    double prod = 1.0;
+    for (int t = 0; t < lgM; ++t) {
+      const double bp = 1.0 / (1.0 + exp(a[t]));
+      prod *= ((m >> (lgM - 1 - t)) & 1) ? bp : 1.0 - bp;
+    }
+    sp[i] = prod;
+  }
+}
+
+// Normalise each LDPC section (builtin sum, sequential, :313) and scale by
+// c_l (:696) into beta0; thread per (codeword, LDPC section).
+template <typename real>
+__global__ void k_sp_norm(const double* __restrict__ sp, const double* __restrict__ cd, int L, int M, int l0,
+                          int ns, int B, real* __restrict__ beta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * ns) return;
+  const int b = i / ns, lp = i % ns, l = l0 + lp;
+  const double* s = sp + (size_t)i * M;
+  double S = 0.0;
+  for (int m = 0; m < M; ++m) S += s[m];
+  real* o = beta + ((size_t)b * L + l) * M;
+  const double c = cd[l];
+  for (int m = 0; m < M; ++m) o[m] = (real)((s[m] / S) * c);
+}
+
+// beta0 of the sections AMP keeps (:657, :691, :696): (beta / c) * c.
+template <typename real>
+__global__ void k_rescale(real* __restrict__ beta, const double* __restrict__ cd, int L, int M, int l0, int ns,
+                          int B) {
+  const size_t tot = (size_t)B * L * M;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+    const int l = (int)((i / M) % L);
+    if (l >= l0 && l < l0 + ns) continue;
+    const double c = cd[l];
+    beta[i] = (real)(((double)beta[i] / c) * c);
+  }
+}
+
+// Hard decisions of the LDPC output (:486-490): bits = app < 0, MSB first.
+__global__ void k_app_idx(const double* __restrict__ app, int lgM, int ns, int B, int32_t* __restrict__ idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * ns) return;
+  const double* a = app + (size_t)i * lgM;
+  int32_t v = 0;
+  for (int t = 0; t < lgM; ++t) v = (v << 1) | (a[t] < 0.0 ? 1 : 0);
+  idx[i] = v;
+}
+
+// One-hot beta0 (sparc_ldpc.py:832-835): beta[b][l*M + idx[b][l]] = c_l, 0 elsewhere.
+template <typename real>
+__global__ void k_onehot(const int32_t* __restrict__ idx, const double* __restrict__ cd, int L, int M, int B,
+                         real* __restrict__ beta) {
+  const size_t tot = (size_t)B * L * M;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t bl = i / M;
+    const int m = (int)(i % M), l = (int)(bl % L);
+    beta[i] = m == idx[bl] ? (real)cd[l] : (real)0;
+  }
+}
+
+int grid_of(size_t tot) {
+  const size_t g = (tot + 255) / 256;
+  return (int)(g < 65536 ? (g > 0 ? g : 1) : 65536);
+}
+
+int check_glue(sa_ctx* c, int B, int l0, int ns) {
+  if (check_ctx(c)) return SA_ERR_ARG;
+  if (B <= 0 || B > c->Bcap) return fail(SA_ERR_ARG, "batch larger than the context's workspace");
+  if (l0 < 0 || ns <= 0 || l0 + ns > c->L) return fail(SA_ERR_ARG, "section range outside [0, L)");
+  if (!c->power_set) return fail(SA_ERR_ARG, "power allocation not staged");
+  if (c->M < 2) return fail(SA_ERR_UNSUPPORTED, "M < 2 carries no bits");
+  return SA_OK;
+}
+
+// Host-or-device fp64 array of `count` values on the context's device:
+// returns a device pointer (copying host data into the staging buffer).
+int dev_in(sa_ctx* c, const double* p, size_t count, int flags, const double** out) {
+  if (flags & SA_PTR_DEVICE) {
+    *out = p;
+    return SA_OK;
+  }
+  int rc = ensure_stage(c, count);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_stage, p, count * 8, hipMemcpyHostToDevice, c->stream));
+  *out = c->d_stage;
+  return SA_OK;
+}
+
+template <typename real>
+int launch_colsum(sa_ctx* c, const int32_t* d_idx, int ldi, int l0, int ns, const real* base, const double* add,
+                  real* out, int B) {
+  dim3 grid((c->n + 255) / 256, B);
+  k_colsum<real><<<grid, 256, (size_t)ns * sizeof(int32_t), c->stream>>>(
+      (const ushort4*)c->d_fwd, c->d_cd, d_idx, ldi, l0, ns, base, add, out, c->n, std::sqrt((double)c->n));
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -1914,6 +2097,7 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_fwd);
   dev_free(c->d_A);
   dev_free(c->d_c);
+  dev_free(c->d_cd);
   dev_free(c->d_stage);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1968,12 +2152,12 @@ int sa_reserve(sa_ctx* c, int B, int T) {
 
 int sa_stage(sa_ctx* c, int B, const double* y, const double* Pl, const double* beta0) {
   if (check_ctx(c)) return SA_ERR_ARG;
-  if (B <= 0 || !y) return fail(SA_ERR_ARG, "sa_stage: bad arguments");
+  if (B <= 0) return fail(SA_ERR_ARG, "sa_stage: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
   if (rc) return rc;
   if (Pl && (rc = set_power(c, Pl))) return rc;
-  if ((rc = upload(c, c->d_y, y, (size_t)B * c->n))) return rc;
+  if (y && (rc = upload(c, c->d_y, y, (size_t)B * c->n))) return rc;  // NULL: keep the staged y
   if (beta0 && (rc = upload(c, c->d_beta, beta0, (size_t)B * c->L * c->M))) return rc;
   return SA_OK;
 }
@@ -2093,6 +2277,124 @@ int sa_decide(sa_ctx* c, int B, int32_t* idx_out) {
 #undef SA_DEC
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(idx_out, c->d_idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+
+int sa_encode(sa_ctx* c, int B, const int32_t* idx, const double* noise) {
+  if (check_ctx(c)) return SA_ERR_ARG;
+  if (B <= 0 || !idx) return fail(SA_ERR_ARG, "sa_encode: bad arguments");
+  if (!c->power_set) return fail(SA_ERR_ARG, "sa_encode: power allocation not staged");
+  if (c->backend != SA_BACKEND_HADAMARD && c->backend != SA_BACKEND_DENSE) return fail(SA_ERR_ARG, "backend");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
+  if (rc) return rc;
+  for (size_t i = 0; i < (size_t)B * c->L; ++i)
+    if (idx[i] < 0 || idx[i] >= c->M) return fail(SA_ERR_ARG, "sa_encode: index outside [0, M)");
+  HIP_TRY(hipMemcpyAsync(c->d_idx, idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  const double* d_noise = nullptr;
+  if (noise && (rc = dev_in(c, noise, (size_t)B * c->n, 0, &d_noise))) return rc;
+  rc = c->prec == SA_PREC_F64
+           ? launch_colsum<double>(c, c->d_idx, c->L, 0, c->L, nullptr, d_noise, (double*)c->d_y, B)
+           : launch_colsum<float>(c, c->d_idx, c->L, 0, c->L, nullptr, d_noise, (float*)c->d_y, B);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+int sa_stage_onehot(sa_ctx* c, int B, const int32_t* idx) {
+  if (check_ctx(c)) return SA_ERR_ARG;
+  if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_stage_onehot: bad arguments");
+  if (!c->power_set) return fail(SA_ERR_ARG, "sa_stage_onehot: power allocation not staged");
+  for (size_t i = 0; i < (size_t)B * c->L; ++i)
+    if (idx[i] < 0 || idx[i] >= c->M) return fail(SA_ERR_ARG, "sa_stage_onehot: index outside [0, M)");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(c->d_idx, idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  const size_t tot = (size_t)B * c->L * c->M;
+  if (c->prec == SA_PREC_F64)
+    k_onehot<double><<<grid_of(tot), 256, 0, c->stream>>>(c->d_idx, c->d_cd, c->L, c->M, B, (double*)c->d_beta);
+  else
+    k_onehot<float><<<grid_of(tot), 256, 0, c->stream>>>(c->d_idx, c->d_cd, c->L, c->M, B, (float*)c->d_beta);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+int sa_llr(sa_ctx* c, int B, int l0, int ns, double* llr, int flags) {
+  int rc = check_glue(c, B, l0, ns);
+  if (rc) return rc;
+  if (!llr) return fail(SA_ERR_ARG, "sa_llr: llr is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  const int lgM = ilog2(c->M);
+  const size_t cnt = (size_t)B * ns * lgM;
+  double* d_out = llr;
+  if (!(flags & SA_PTR_DEVICE)) {
+    if ((rc = ensure_stage(c, cnt))) return rc;
+    d_out = c->d_stage;
+  }
+  if (c->prec == SA_PREC_F64)
+    k_llr<double><<<grid_of(cnt), 256, 0, c->stream>>>((const double*)c->d_beta, c->d_cd, c->L, c->M, lgM, l0, ns, B, d_out);
+  else
+    k_llr<float><<<grid_of(cnt), 256, 0, c->stream>>>((const float*)c->d_beta, c->d_cd, c->L, c->M, lgM, l0, ns, B, d_out);
+  HIP_TRY(hipGetLastError());
+  if (!(flags & SA_PTR_DEVICE)) HIP_TRY(hipMemcpyAsync(llr, d_out, cnt * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+int sa_soft_beta0(sa_ctx* c, int B, int l0, int ns, const double* app, int flags) {
+  int rc = check_glue(c, B, l0, ns);
+  if (rc) return rc;
+  if (!app) return fail(SA_ERR_ARG, "sa_soft_beta0: app is NULL");
+  HIP_TRY(hipSetDevice(c->device));
+  const int lgM = ilog2(c->M);
+  const size_t na = (size_t)B * ns * lgM, nsp = (size_t)B * ns * c->M;
+  // staging layout: [app copy (host input only)] [sp]
+  const size_t off = (flags & SA_PTR_DEVICE) ? 0 : na;
+  if ((rc = ensure_stage(c, off + nsp))) return rc;
+  const double* d_app = app;
+  if (!(flags & SA_PTR_DEVICE)) {
+    HIP_TRY(hipMemcpyAsync(c->d_stage, app, na * 8, hipMemcpyHostToDevice, c->stream));
+    d_app = c->d_stage;
+  }
+  double* sp = c->d_stage + off;
+  k_bp2sp<<<grid_of(nsp), 256, 0, c->stream>>>(d_app, c->M, lgM, ns, B, sp);
+  const int nb = (B * ns + 255) / 256;
+  const size_t tot = (size_t)B * c->L * c->M;
+  if (c->prec == SA_PREC_F64) {
+    k_rescale<double><<<grid_of(tot), 256, 0, c->stream>>>((double*)c->d_beta, c->d_cd, c->L, c->M, l0, ns, B);
+    k_sp_norm<double><<<nb, 256, 0, c->stream>>>(sp, c->d_cd, c->L, c->M, l0, ns, B, (double*)c->d_beta);
+  } else {
+    k_rescale<float><<<grid_of(tot), 256, 0, c->stream>>>((float*)c->d_beta, c->d_cd, c->L, c->M, l0, ns, B);
+    k_sp_norm<float><<<nb, 256, 0, c->stream>>>(sp, c->d_cd, c->L, c->M, l0, ns, B, (float*)c->d_beta);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+int sa_hard_cancel(sa_ctx* c, int B, int l0, int ns, const double* app, int flags, sa_ctx* dst, int32_t* idx_out) {
+  int rc = check_glue(c, B, l0, ns);
+  if (rc) return rc;
+  if (!app) return fail(SA_ERR_ARG, "sa_hard_cancel: app is NULL");
+  if (dst && (dst->n != c->n || dst->prec != c->prec || dst->device != c->device))
+    return fail(SA_ERR_ARG, "sa_hard_cancel: dst must share n, precision and device");
+  HIP_TRY(hipSetDevice(c->device));
+  if (dst && (rc = ensure_workspace(dst, B, dst->Tcap > 0 ? dst->Tcap : 1))) return rc;
+  const int lgM = ilog2(c->M);
+  const double* d_app = nullptr;
+  if ((rc = dev_in(c, app, (size_t)B * ns * lgM, flags, &d_app))) return rc;
+  k_app_idx<<<(B * ns + 255) / 256, 256, 0, c->stream>>>(d_app, lgM, ns, B, c->d_idx);
+  HIP_TRY(hipGetLastError());
+  if (dst) {
+    rc = c->prec == SA_PREC_F64
+             ? launch_colsum<double>(c, c->d_idx, ns, l0, ns, (const double*)c->d_y, nullptr, (double*)dst->d_y, B)
+             : launch_colsum<float>(c, c->d_idx, ns, l0, ns, (const float*)c->d_y, nullptr, (float*)dst->d_y, B);
+    if (rc) return rc;
+  }
+  if (idx_out)
+    HIP_TRY(hipMemcpyAsync(idx_out, c->d_idx, (size_t)B * ns * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }

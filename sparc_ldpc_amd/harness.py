@@ -44,8 +44,7 @@ class SPARCParams:
 
 
 class LDPCParams:
-    """sparc_ldpc.py:250-255 (same fields).  The outer LDPC code is a later
-    row of the build; passing one raises NotImplementedError."""
+    """sparc_ldpc.py:250-255 (same fields); consumed by sparc_ldpc_amd.joint."""
 
     def __init__(self, standard, r_ldpc, z, ptype='A'):
         self.standard = standard
@@ -92,14 +91,15 @@ def ber_of(sent, decided, total_bits):
 
 def amp_ldpc_sim(sparcparams: SPARCParams, ldpcparams=None, a=None, f=None, C=None, *,
                  backend=None, precision=None):
-    """Plain-SPARC branch of sparc_ldpc.py:359-545: one Monte-Carlo rep.
-
-    Returns (ber_amp, None, None, R) like the reference with ldpcparams=None.
+    """sparc_ldpc.py:359-545: one Monte-Carlo rep.  With an LDPC code this is
+    the original hard exchange (``joint.amp_ldpc_sim_ldpc``); without one,
+    plain SPARC returning (ber_amp, None, None, R) like the reference.
     Draw order of np.random: randint(0, 2, total_bits) (:423-424), then
     randn(n, 1) (:445).
     """
     if ldpcparams is not None:
-        raise NotImplementedError("outer LDPC code: SURVEY §8f next row (not in this build yet)")
+        from .joint import amp_ldpc_sim_ldpc
+        return amp_ldpc_sim_ldpc(sparcparams, ldpcparams, backend=backend, precision=precision)
     L, M, P = sparcparams.L, sparcparams.M, sparcparams.p
     sigma, r_sparc, T = sparcparams.sigma, sparcparams.r, sparcparams.t
     a, f, C = sparcparams.a, sparcparams.f, sparcparams.C

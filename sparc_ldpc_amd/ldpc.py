@@ -32,6 +32,7 @@ EXPORTS = (
     "sumprod", "sumprod2", "minsum", "Lxor", "Lxfb",
     "lb_create", "lb_destroy", "lb_decode", "lb_decode_device", "lb_stage", "lb_run", "lb_wait",
     "lb_fetch", "lb_run_event_ms", "lb_info", "lb_device_count", "lb_last_error", "lb_version",
+    "lb_buffers",
 )
 
 _P, _I, _D = ct.c_void_p, ct.c_int, ct.POINTER(ct.c_double)
@@ -47,6 +48,7 @@ _SIG = {
     "lb_decode": (_I, [_P, _I, _D, _D, ct.POINTER(ct.c_int), _I, ct.c_double, _I]),
     "lb_decode_device": (_I, [_P, _I, _P, _P, _P, _I, ct.c_double, _I]),
     "lb_stage": (_I, [_P, _I, _D]),
+    "lb_buffers": (_I, [_P, _I, ct.POINTER(_P), ct.POINTER(_P), ct.POINTER(_P)]),
     "lb_run": (_I, [_P, _I, _I, ct.c_double, _I]),
     "lb_wait": (_I, [_P]),
     "lb_fetch": (_I, [_P, _I, _D, ct.POINTER(ct.c_int)]),
@@ -261,6 +263,26 @@ class code:
                              it.ctypes.data_as(ct.POINTER(ct.c_int)), _ALGOS[dectype],
                              float(corr_factor), int(max_iter)))
         return app, it.astype(np.int64)
+
+    def device_buffers(self, B):
+        """Device pointers (ch, app, iters) of the decoder's buffers for B words."""
+        ch, app, it = ct.c_void_p(), ct.c_void_p(), ct.c_void_p()
+        _check(load_bp_library().lb_buffers(self._context(), int(B), ct.byref(ch), ct.byref(app), ct.byref(it)))
+        return ch.value, app.value, it.value
+
+    def run_buffers(self, B, dectype="sumprod2", corr_factor=0.7, max_iter=MAX_ITCOUNT):
+        """Decode the B words in the device ch buffer into the app buffer (blocking)."""
+        lib = load_bp_library()
+        _check(lib.lb_run(self._context(), int(B), _ALGOS[dectype], float(corr_factor), int(max_iter)))
+        _check(lib.lb_wait(self._context()))
+
+    def fetch_buffers(self, B, app=True):
+        """(app (B, N) or None, iters (B,)) from the device buffers."""
+        a = np.empty((B, self.Nv)) if app else None
+        it = np.empty(B, dtype=np.intc)
+        _check(load_bp_library().lb_fetch(self._context(), int(B), None if a is None else a.ctypes.data_as(_D),
+                                          it.ctypes.data_as(ct.POINTER(ct.c_int))))
+        return a, it.astype(np.int64)
 
     def decode(self, ch, dectype="sumprod2", corr_factor=0.7):
         """ldpc.py:855-930: (app, it) for one word of channel LLRs."""

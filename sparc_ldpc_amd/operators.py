@@ -210,6 +210,69 @@ class SparcOperator:
         keys = ("L", "M", "n", "w", "backend", "precision", "device", "device_bytes")
         return dict(zip(keys, (int(v) for v in o)))
 
+    # ---- SPARC <-> LDPC glue (device kernels, include/sparc_amp.h) ----------
+    # llr / app arguments: a host float64 array, or an int device pointer
+    # (e.g. the LDPC decoder's buffers from ldpc.code.device_buffers).
+    @staticmethod
+    def _ptr(x):
+        if isinstance(x, int):
+            return _lib.ct.c_void_p(x), _lib.SA_PTR_DEVICE
+        return _lib.ct.c_void_p(x.ctypes.data), 0
+
+    def stage_power(self, B, Pl):
+        """Stage the section powers (c_l = sqrt(n Pl_l)) for a batch of B."""
+        Pl = as_f64(Pl).reshape(-1)
+        assert Pl.size == self.L, "Pl must hold L section powers"
+        check(self._lib.sa_stage(self._ctx, int(B), None, dptr(Pl), None))
+
+    def encode(self, idx, noise=None):
+        """Stage y = A β(idx) + noise (sparc_ldpc.py:436-446); idx (B, L) section indices."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        B = idx.shape[0]
+        assert idx.shape == (B, self.L)
+        nz = None
+        if noise is not None:
+            noise = as_f64(noise)
+            assert noise.size == B * self.n
+            nz = dptr(noise)
+        check(self._lib.sa_encode(self._ctx, B, idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32)), nz))
+        return B
+
+    def stage_onehot(self, idx):
+        """Stage the one-hot β₀ of section indices idx (B, L) for run(..., beta0=True)."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        check(self._lib.sa_stage_onehot(self._ctx, idx.shape[0],
+                                        idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
+
+    def llr(self, B, l0, ns, out=None):
+        """LDPC-bit LLRs of sections [l0, l0+ns) of the current β (sparc_ldpc.py:470-479).
+        out: None (returns a (B, ns*log2 M) array) or a device pointer."""
+        lgm = int(np.log2(self.M))
+        if out is None:
+            out = np.empty((B, ns * lgm))
+        p, fl = self._ptr(out)
+        check(self._lib.sa_llr(self._ctx, int(B), int(l0), int(ns), p, fl))
+        return out
+
+    def soft_beta0(self, B, l0, ns, app):
+        """Stage β₀ = β with sections [l0, l0+ns) from the LDPC app (sparc_ldpc.py:683-698)."""
+        if not isinstance(app, int):
+            app = as_f64(app)
+        p, fl = self._ptr(app)
+        check(self._lib.sa_soft_beta0(self._ctx, int(B), int(l0), int(ns), p, fl))
+
+    def hard_cancel(self, B, l0, ns, app, dst=None):
+        """Hard LDPC decisions of sections [l0, l0+ns) -> (B, ns) indices; with dst,
+        stage y - A β_hard as dst's input (sparc_ldpc.py:486-524)."""
+        if not isinstance(app, int):
+            app = as_f64(app)
+        p, fl = self._ptr(app)
+        idx = np.empty((B, ns), dtype=np.int32)
+        check(self._lib.sa_hard_cancel(self._ctx, int(B), int(l0), int(ns), p, fl,
+                                       None if dst is None else dst.ctx,
+                                       idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
+        return idx
+
     def subset(self, sections) -> "SparcOperator":
         """Operator over the given parent sections (sparc_transforms_shorter)."""
         sec = np.ascontiguousarray(np.asarray(sections, dtype=np.int64).reshape(-1))

@@ -4,6 +4,11 @@
   plain   : waterfall()'s BER_plain column (sparc_ldpc.py:1126-1282):
             L=M=512 P=4 R=5/6 T=64, Eb/N0 = linspace(3, 10, 10) dB (20*log10),
             MIN_ERRORS=200 / MAX_BLOCKS=250.
+  soft / hard / originalHard : the joint waterfall() runs (configs[4]):
+            L=M=512 P=4 r_sparc=1 T=64 with the 802.16 rate-5/6 outer code
+            (all 512 sections; originalHard: 384 as the shipped call), every
+            BER column incl. plain SPARC and LDPC+BPSK, MIN_ERRORS=200 /
+            MAX_BLOCKS=250.
   l768    : soft_hard_plot()'s BER_sparc column (sparc_ldpc.py:1285-1432):
             L=768 M=512 P=1.8 at the overall rate R=0.8765 (sec=569),
             sigma = linspace(0.8, 0.4, 10), 100 reps per point.
@@ -25,11 +30,11 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sweep", default="plain", choices=["plain", "l768"])
+    ap.add_argument("--sweep", default="plain", choices=["plain", "l768", "soft", "hard", "originalHard"])
     ap.add_argument("--points", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--out", default="gpurun_out/waterfall")
-    ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--precision", default=None, help="fp32 | fp64 (default: fp32 plain sweeps, fp64 joint)")
     args = ap.parse_args()
     import sparc_ldpc_amd as sp
     from sparc_ldpc_amd import dist
@@ -43,11 +48,24 @@ def main():
         rows = sp.waterfall_plain(cfg["L"], cfg["M"], cfg["P"], cfg["R"], cfg["T"], ebno,
                                   cfg["MIN_ERRORS"], cfg["MAX_BLOCKS"],
                                   csv_filename=args.out + ".csv" if rank == 0 else None,
-                                  batch=args.batch, precision=args.precision, rank=rank, world=world,
+                                  batch=args.batch, precision=args.precision or "fp32", rank=rank, world=world,
                                   allreduce=dist.allreduce_sum)
         ref = pub["waterfall_plain"]["BER_plain_runs"]
         for i, r in enumerate(rows):
             r["reference_runs"] = [v[i] for v in ref.values()]
+    elif args.sweep in ("soft", "hard", "originalHard"):
+        cfg = pub["waterfall_joint"]["config"]
+        sections = 384 if args.sweep == "originalHard" else 512
+        spp = sp.SPARCParams(cfg["L"], cfg["M"], None, cfg["P"], cfg["r_sparc"], cfg["T"])
+        lp = sp.LDPCParams("802.16", "5/6", None)
+        ebno = np.linspace(3, 10, 10)[:args.points]
+        rows = sp.waterfall(spp, lp, csv_filename=args.out + ".csv" if rank == 0 else None, init=args.sweep,
+                            MIN_ERRORS=cfg["MIN_ERRORS"], MAX_BLOCKS=cfg["MAX_BLOCKS"], sections=sections,
+                            batch=args.batch, precision=args.precision, rank=rank, world=world,
+                            allreduce=dist.allreduce_sum, ebno_dbs=ebno)
+        ref = pub["waterfall_joint"]["runs"][args.sweep]
+        for i, r in enumerate(rows):
+            r["reference"] = {k: ref[k][i] for k in ref if k not in ("file", "EbN0_dB")}
     else:
         cfg = pub["soft_hard_BER_sparc"]["config"]
         L, M, P, T = cfg["L"], cfg["M"], cfg["P"], cfg["T"]
@@ -55,7 +73,7 @@ def main():
         n_coded = L * logm / 1
         R = (L * logm - 9 * 569 * (1 - 5 / 6)) / n_coded
         n = int(L * logm / R)
-        op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=args.precision)
+        op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=args.precision or "fp32")
         Pl = P / L * np.ones(L)
         rows = []
         for i, sigma in enumerate(np.linspace(0.8, 0.4, 10)[:args.points]):

@@ -196,7 +196,15 @@ _JD_CACHE: "OrderedDict[tuple, JointDecoder]" = OrderedDict()
 
 
 def joint_decoder(L, M, n, ldpcparams: LDPCParams, T, backend=None, precision=None, device=None):
-    """Cached JointDecoder (the operator tables and the LDPC graph are built once)."""
+    """Cached JointDecoder (the operator tables and the LDPC graph are built once).
+
+    AMP runs in binary64 unless told otherwise: in fp32 the softmax of the
+    denoiser underflows below e^-87 (fp64: e^-745), so confident sections
+    give p in {0, 1} exactly and the LLRs saturate at +-DBL_MAX, including
+    for wrong decisions that BP could otherwise revise (measured: the fp32
+    soft waterfall's BER_ldpc stalls near 0.4 above 7 dB, the fp64 one
+    overlays the reference's published curve)."""
+    precision = precision or "fp64"
     key = (L, M, n, ldpcparams.standard, ldpcparams.r_ldpc, ldpcparams.z, ldpcparams.ptype, T,
            backend, precision, device)
     jd = _JD_CACHE.get(key)
@@ -308,6 +316,7 @@ def waterfall(sparcparams: SPARCParams, ldpcparams: LDPCParams, csv_filename=Non
     BER_bpsk from sim_ldpc.  Reps are sharded over ranks like ber_point.
     Returns the rows; writes the reference CSV schema (:1257-1264) on rank 0."""
     from .harness import mc_decode
+    precision = precision or "fp64"  # see joint_decoder
     L, M = sparcparams.L, sparcparams.M
     logm = int(np.log2(M))
     p, r_sparc, T = sparcparams.p, sparcparams.r, sparcparams.t

@@ -26,3 +26,26 @@ def test_plain_waterfall_overlays_reference(lib_gpu):
         lo, hi = runs[:, i].min() / 1.5, runs[:, i].max() * 1.5
         assert lo <= r["BER_plain"] <= hi, (r["EbN0_dB"], r["BER_plain"], lo, hi)
         assert r["blocks"] <= c["MAX_BLOCKS"]
+
+
+@pytest.mark.parametrize("init", ["soft", "hard"])
+def test_joint_waterfall_overlays_reference(lib_gpu, init):
+    """configs[4]: L=M=512 with the 802.16 rate-5/6 code over all sections,
+    AMP <-> BP exchange; the points where every column is >= 1e-3 (3.0 and
+    6.89 dB) fall within 1.5x of the reference run of the same scheme."""
+    import sparc_ldpc_amd as sp
+    with open(os.path.join(GOLDEN, "published_ber.json")) as fh:
+        pub = json.load(fh)["waterfall_joint"]
+    c = pub["config"]
+    ref = pub["runs"][init]
+    pts = [0, 5]
+    ebno = np.linspace(3, 10, 10)[pts]
+    spp = sp.SPARCParams(c["L"], c["M"], None, c["P"], c["r_sparc"], c["T"])
+    rows = sp.waterfall(spp, sp.LDPCParams("802.16", "5/6", None), init=init, MIN_ERRORS=c["MIN_ERRORS"],
+                        MAX_BLOCKS=c["MAX_BLOCKS"], bpsk=True, batch=64, ebno_dbs=ebno)
+    for i, r in zip(pts, rows):
+        for col in ("BER_amp_1", "BER_ldpc", "BER_amp_2", "BER_plain"):
+            lo, hi = ref[col][i] / 1.5, ref[col][i] * 1.5
+            assert lo <= r[col] <= hi, (init, r["EbN0_dB"], col, r[col], ref[col][i])
+        if i == 0:
+            assert ref["BER_bpsk"][i] / 1.5 <= r["BER_bpsk"] <= ref["BER_bpsk"][i] * 1.5

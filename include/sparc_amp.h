@@ -143,6 +143,18 @@ int sa_soft_beta0(sa_ctx* ctx, int B, int l0, int ns, const double* app, int fla
 int sa_hard_cancel(sa_ctx* ctx, int B, int l0, int ns, const double* app, int flags, sa_ctx* dst,
                    int32_t* idx_out);
 
+/* Threshold decisions (amp_exit.py:56-105): for sections [l0, l0+ns) the
+ * bp2sp of the LLRs `app` ([B][ns*log2 M]); idx_out[b][s] = the entry whose
+ * normalised probability exceeds `threshold` if exactly one does, else -1. */
+int sa_threshold(sa_ctx* ctx, int B, int l0, int ns, const double* app, int flags, double threshold,
+                 int32_t* idx_out);
+
+/* Hard cancellation of decided sections (amp_exit.py:107-109): stages
+ * y - A beta(idx) as dst's input y, idx [B][L] with -1 for sections that are
+ * not cancelled; dst is a context over the same n (e.g. sa_subset of the
+ * undecided sections). */
+int sa_cancel(sa_ctx* ctx, int B, const int32_t* idx, sa_ctx* dst);
+
 /* Introspection. */
 int sa_info(const sa_ctx* ctx, int64_t* out8); /* L, M, n, w, backend, precision, device, bytes */
 int sa_device_count(void);

@@ -443,13 +443,16 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   if ((rc = dev_alloc((void**)&c->d_vedge, vedge.size() * sizeof(int)))) return bail(rc);
   if ((rc = dev_alloc((void**)&c->d_vdeg, (size_t)Nv))) return bail(rc);
   if ((rc = dev_alloc((void**)&c->d_cstart, (size_t)(Nc + 1) * sizeof(int)))) return bail(rc);
-  if (hipMemcpy(c->d_vedge, vedge.data(), vedge.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_vdeg, vd.data(), (size_t)Nv, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_cstart, cs.data(), (size_t)(Nc + 1) * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
-    return bail(fail(LB_ERR_HIP, "graph upload failed"));
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(LB_ERR_HIP, "stream/event creation failed"));
+  // uploads on the context's non-blocking stream, waited for (a pageable
+  // hipMemcpy may return before its DMA lands, unordered with this stream)
+  if (hipMemcpyAsync(c->d_vedge, vedge.data(), vedge.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(c->d_vdeg, vd.data(), (size_t)Nv, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(c->d_cstart, cs.data(), (size_t)(Nc + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return bail(fail(LB_ERR_HIP, "graph upload failed"));
   *out = c;
   return LB_OK;
 }

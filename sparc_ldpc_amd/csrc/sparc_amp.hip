@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -304,7 +305,8 @@ struct SecArgs {
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   const real* __restrict__ c;        // [L]     sqrt(n * Pl)
   const real* __restrict__ z;        // [B][n]
-  real* __restrict__ beta;           // [B][L*M]
+  real* __restrict__ beta;           // [B][L*M] previous estimate (read)
+  real* __restrict__ beta_out;       // [B][L*M] new estimate (k_sec: the other ping-pong buffer)
   real* __restrict__ out;            // [B][L*M] (SEC_AZ)
   real* __restrict__ abp;            // [B][G][n] partial sums of Ab over this group's sections
   real* __restrict__ bbp;            // [B][G]    partial sums of beta^2
@@ -419,6 +421,10 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
   real v[E];
   real bprev[E];
   real* bl = a.beta + (size_t)b * LM + (size_t)lc * M;
+  // The RS workgroups of a group all read beta_l(t) while the owner writes
+  // beta_l(t+1): the two live in different buffers (ping-pong), otherwise a
+  // late reader would see the new estimate.
+  real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M;
   const uint16_t* il = a.inv + (size_t)lc * a.w;
   const ushort4* fw = a.fwd + (size_t)g * n;
   ushort4 tb[KH][NQ];
@@ -510,7 +516,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
       return;  // uniform: no barrier follows in this mode
     }
     if (have) {
-      const real bb = denoise_section<real, E>(v, bprev, bl, lane, M, cl, tau2, a.sqrt_n, owner);
+      const real bb = denoise_section<real, E>(v, bprev, blo, lane, M, cl, tau2, a.sqrt_n, owner);
       if (lane == 0) bbw[wv] = bb;  // per-wave beta^2, summed below in section order
   STAMP(5);
     }
@@ -1041,6 +1047,21 @@ __global__ void k_convert(const src_t* s, dst_t* d, size_t N) {
     d[i] = (dst_t)s[i];
 }
 
+// Word fill used inside captured sequences instead of hipMemsetAsync (keeps
+// the graphs made of kernel nodes only).
+__global__ void k_fill32(uint32_t* p, uint32_t v, size_t nw) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+template <typename real>
+__global__ void k_beta_final(real* beta, const real* beta2, const int* it, size_t LM) {
+  const int b = blockIdx.y;
+  if (!(it[b] & 1)) return;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < LM; i += (size_t)gridDim.x * blockDim.x)
+    beta[(size_t)b * LM + i] = beta2[(size_t)b * LM + i];
+}
+
 __global__ void k_iters_final(int* it, int B, int T) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B && it[b] < 0) it[b] = T;
@@ -1282,6 +1303,8 @@ struct sa_ctx {
   double* d_stage = nullptr;
   size_t stage_cap = 0;
   double* d_cd = nullptr;  // c_l = sqrt(n Pl_l) in binary64 (joint-decoding glue)
+  void* d_beta2 = nullptr;  // ping-pong partner of d_beta for k_sec (B x L*M), sized beta2_cap
+  int beta2_cap = 0;
   double P = 0;
   bool power_set = false;
   size_t bytes = 0;
@@ -1322,6 +1345,8 @@ void free_workspace(sa_ctx* c) {
   }
   dev_free(c->d_iters); c->d_iters = nullptr;
   dev_free(c->d_idx); c->d_idx = nullptr;
+  dev_free(c->d_beta2); c->d_beta2 = nullptr;
+  c->beta2_cap = 0;
   c->Bcap = c->Tcap = 0;
 }
 
@@ -1350,6 +1375,19 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
     if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->RS * c->lda * sizeof(float)))) return rc;
   c->Bcap = nB;
   c->Tcap = nT;
+  // Debug aid: SPARC_AMP_POISON=<mask> fills the workspace with 0xFF bytes
+  // (NaN) so a read of a value the decode never wrote shows up.
+  if (const char* pz = getenv("SPARC_AMP_POISON")) {
+    const int mask = atoi(pz);
+    const size_t LMs = (size_t)c->L * c->M * s;
+    void* bufs[] = {c->d_y, c->d_z, c->d_beta, c->d_out, c->d_abp, c->d_bbp, c->d_zzp, c->d_tau};
+    const size_t sz[] = {nB * c->n * s, nB * c->n * s, nB * LMs, nB * (LMs > (size_t)c->n * s ? LMs : (size_t)c->n * s),
+                         (size_t)nB * Gmax * c->n * s, (size_t)nB * (c->G > c->Gd ? c->G : c->Gd) * s,
+                         (size_t)nB * c->NZ * s, (size_t)nB * (nT + 1) * s};
+    for (int i = 0; i < 8; ++i)
+      if (mask & (1 << i)) HIP_TRY(hipMemsetAsync(bufs[i], 0xff, sz[i], c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
   return SA_OK;
 }
 
@@ -1397,7 +1435,7 @@ template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
   a.inv = c->d_inv; a.fwd = (const ushort4*)c->d_fwd; a.c = (const real*)c->d_c;
-  a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.out = (real*)c->d_out;
+  a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
   a.L = c->L; a.M = c->M; a.n = c->n; a.w = c->w; a.nhi = c->nhi; a.G = c->G; a.NZ = c->NZ;
@@ -1485,8 +1523,10 @@ int launch_secb(sa_ctx* c, int B, int t, int es) {
 bool use_batched(const sa_ctx* c, int B) { return c->CB > 0 && B >= 4; }
 
 template <typename real>
-int launch_sec(sa_ctx* c, int B, int mode, int t, int es) {
+int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, void* bout = nullptr) {
   SecArgs<real> a = sec_args<real>(c, mode, t, es);
+  if (bin) a.beta = (real*)bin;
+  if (bout) a.beta_out = (real*)bout;
   switch (c->E) {
     case 1: launch_sec_e<real, 1>(c, B, a); break;
     case 2: launch_sec_e<real, 2>(c, B, a); break;
@@ -1617,7 +1657,7 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const int G = dense ? c->KS : (batched ? c->Gb : c->G);
   const int Gb = dense ? c->Gd : (batched ? c->Gb : c->G);
   int rc;
-  HIP_TRY(hipMemsetAsync(c->d_iters, 0xff, (size_t)B * sizeof(int), c->stream));
+  k_fill32<<<(B + 255) / 256, 256, 0, c->stream>>>((uint32_t*)c->d_iters, 0xffffffffu, (size_t)B);
   if (has_b0) {
     if (dense) {
       if ((rc = launch_dense_ab(c, B, 0, 0, 1))) return rc;
@@ -1627,7 +1667,8 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
       if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, c->G, c->G))) return rc;
     }
   } else {
-    HIP_TRY(hipMemsetAsync(c->d_beta, 0, (size_t)B * c->L * c->M * rsz(c), c->stream));
+    const size_t nw = (size_t)B * c->L * c->M * rsz(c) / 4;
+    k_fill32<<<(int)std::min<size_t>((nw + 255) / 256, 8192), 256, 0, c->stream>>>((uint32_t*)c->d_beta, 0u, nw);
     if ((rc = launch_row<real>(c, B, ROW_INIT0, 0, 0, G, Gb))) return rc;
   }
   for (int t = 0; t < T; ++t) {
@@ -1638,17 +1679,50 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     } else if (batched) {
       if ((rc = launch_secb<real>(c, B, t, es))) return rc;
     } else {
-      if ((rc = launch_sec<real>(c, B, SEC_AMP, t, es))) return rc;
+      void* pin = (t & 1) ? c->d_beta2 : c->d_beta;
+      void* pout = (t & 1) ? c->d_beta : c->d_beta2;
+      if ((rc = launch_sec<real>(c, B, SEC_AMP, t, es, pin, pout))) return rc;
     }
     if ((rc = launch_row<real>(c, B, ROW_AMP, t, es, G, Gb))) return rc;
   }
   k_iters_final<<<(B + 255) / 256, 256, 0, c->stream>>>(c->d_iters, B, T);
   HIP_TRY(hipGetLastError());
+  if (!dense && !batched && T > 0) {
+    // the estimate of codeword b is in the buffer of parity iters[b]
+    const size_t LM = (size_t)c->L * c->M;
+    k_beta_final<real><<<dim3((unsigned)std::min<size_t>((LM + 255) / 256, 4096), B), 256, 0, c->stream>>>(
+        (real*)c->d_beta, (const real*)c->d_beta2, c->d_iters, LM);
+    HIP_TRY(hipGetLastError());
+  }
+  return SA_OK;
+}
+
+int ensure_beta2(sa_ctx* c, int B) {
+  if (c->backend == SA_BACKEND_DENSE || use_batched(c, B) || c->beta2_cap >= c->Bcap) return SA_OK;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  dev_free(c->d_beta2);
+  c->d_beta2 = nullptr;
+  c->beta2_cap = 0;
+  int rc = dev_alloc(c, &c->d_beta2, (size_t)c->Bcap * c->L * c->M * rsz(c));
+  if (rc) return rc;
+  c->beta2_cap = c->Bcap;
+  drop_graphs(c);  // captured graphs hold the old pointer
   return SA_OK;
 }
 
 template <typename real>
 int run_graph(sa_ctx* c, int B, int T, int flags, int has_b0) {
+  int rc0 = ensure_beta2(c, B);
+  if (rc0) return rc0;
+  if (getenv("SPARC_AMP_NO_GRAPH")) {  // debug aid: eager launches instead of the captured graph
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    int rc = seq_amp<real>(c, B, T, flags, has_b0);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    c->last_B = B;
+    c->last_T = T;
+    return SA_OK;
+  }
   const auto key = std::make_tuple(B, T, flags, has_b0);
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
@@ -1725,8 +1799,12 @@ int build_tables(sa_ctx* c) {
   int rc;
   if ((rc = dev_alloc(c, (void**)&c->d_inv, inv.size() * 2))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_fwd, fwd.size() * 2))) return rc;
-  HIP_TRY(hipMemcpy(c->d_inv, inv.data(), inv.size() * 2, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(c->d_fwd, fwd.data(), fwd.size() * 2, hipMemcpyHostToDevice));
+  // On the context's (non-blocking) stream and waited for: a pageable
+  // hipMemcpy may return once the data is staged, before the DMA lands, and
+  // the null stream does not order the kernels of a non-blocking stream.
+  HIP_TRY(hipMemcpyAsync(c->d_inv, inv.data(), inv.size() * 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_fwd, fwd.data(), fwd.size() * 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
 
@@ -1737,7 +1815,7 @@ int build_dense(sa_ctx* c) {
   if ((rc = dev_alloc(c, (void**)&c->d_A, (size_t)n * c->lda * sizeof(float)))) return rc;
   uint32_t* d_ord = nullptr;
   HIP_TRY(hipMalloc(&d_ord, c->ordering.size() * 4));
-  HIP_TRY(hipMemcpy(d_ord, c->ordering.data(), c->ordering.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpyAsync(d_ord, c->ordering.data(), c->ordering.size() * 4, hipMemcpyHostToDevice, c->stream));
   const float s = (float)(1.0 / std::sqrt((double)n));
   k_dense_build<<<8192, 256, 0, c->stream>>>(d_ord, c->d_A, L, M, n, w, c->lda, s);
   hipError_t e = hipGetLastError();
@@ -1921,7 +1999,7 @@ __global__ void __launch_bounds__(256) k_colsum(const ushort4* __restrict__ fwd,
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int l = g * kSpw + q;
-      if (l < l0 || l >= l0 + ns) continue;
+      if (l < l0 || l >= l0 + ns || sidx[l - l0] < 0) continue;  // idx < 0: section not decided
       const unsigned k = fq[q] & 0x7fffu;
       const unsigned neg = (fq[q] >> 15) ^ (__popc(k & (unsigned)sidx[l - l0]) & 1u);
       acc += neg ? -cd[l] : cd[l];
@@ -2024,6 +2102,43 @@ __global__ void k_onehot(const int32_t* __restrict__ idx, const double* __restri
     const int m = (int)(i % M), l = (int)(bl % L);
     beta[i] = m == idx[bl] ? (real)cd[l] : (real)0;
   }
+}
+
+// Threshold decisions of the LDPC soft output (amp_exit.py:56-105 on the
+// bp2sp of sparc_ldpc.py:987-994): per (codeword, section) the normalised
+// product of bit marginals sp_m / S; the section is decided (index m) iff
+// exactly one entry exceeds the threshold, else -1.  One workgroup per
+// section: products in LDS, the reference's sequential normaliser, counts.
+__global__ void __launch_bounds__(256) k_threshold(const double* __restrict__ app, int M, int lgM, int ns,
+                                                   double thr, int32_t* __restrict__ idx) {
+  extern __shared__ double sp[];
+  __shared__ int cnt, pick;
+  __shared__ double S;
+  const size_t bl = blockIdx.x;  // b * ns + section
+  const double* a = app + bl * lgM;
+  for (int m = threadIdx.x; m < M; m += 256) {
+    double prod = 1.0;
+    for (int t = 0; t < lgM; ++t) {
+      const double bp = 1.0 / (1.0 + exp(a[t]));
+      prod *= ((m >> (lgM - 1 - t)) & 1) ? bp : 1.0 - bp;
+    }
+    sp[m] = prod;
+  }
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int m = 0; m < M; ++m) s += sp[m];
+    S = s;
+  }
+  __syncthreads();
+  for (int m = threadIdx.x; m < M; m += 256)
+    if (sp[m] / S > thr) {
+      atomicAdd(&cnt, 1);
+      pick = m;  // only read when cnt == 1
+    }
+  __syncthreads();
+  if (threadIdx.x == 0) idx[bl] = cnt == 1 ? pick : -1;
 }
 
 int grid_of(size_t tot) {
@@ -2226,6 +2341,7 @@ int sa_profile(sa_ctx* c, int B, int T, int flags, double* out) {
     return fail(SA_ERR_ARG, "sa_profile: bad arguments (reserve and stage first)");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int rcb = ensure_beta2(c, B)) return rcb;
   Prof prof;
   c->prof = &prof;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -2395,6 +2511,42 @@ int sa_hard_cancel(sa_ctx* c, int B, int l0, int ns, const double* app, int flag
   }
   if (idx_out)
     HIP_TRY(hipMemcpyAsync(idx_out, c->d_idx, (size_t)B * ns * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+int sa_threshold(sa_ctx* c, int B, int l0, int ns, const double* app, int flags, double threshold,
+                 int32_t* idx_out) {
+  int rc = check_glue(c, B, l0, ns);
+  if (rc) return rc;
+  if (!app || !idx_out) return fail(SA_ERR_ARG, "sa_threshold: null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  const int lgM = ilog2(c->M);
+  const double* d_app = nullptr;
+  if ((rc = dev_in(c, app, (size_t)B * ns * lgM, flags, &d_app))) return rc;
+  k_threshold<<<B * ns, 256, (size_t)c->M * sizeof(double), c->stream>>>(d_app, c->M, lgM, ns, threshold, c->d_idx);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(idx_out, c->d_idx, (size_t)B * ns * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+int sa_cancel(sa_ctx* c, int B, const int32_t* idx, sa_ctx* dst) {
+  if (check_ctx(c) || check_ctx(dst)) return SA_ERR_ARG;
+  if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_cancel: bad arguments");
+  if (!c->power_set) return fail(SA_ERR_ARG, "sa_cancel: power allocation not staged");
+  if (dst->n != c->n || dst->prec != c->prec || dst->device != c->device)
+    return fail(SA_ERR_ARG, "sa_cancel: dst must share n, precision and device");
+  for (size_t i = 0; i < (size_t)B * c->L; ++i)
+    if (idx[i] >= c->M) return fail(SA_ERR_ARG, "sa_cancel: index >= M");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_workspace(dst, B, dst->Tcap > 0 ? dst->Tcap : 1))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_idx, idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  rc = c->prec == SA_PREC_F64
+           ? launch_colsum<double>(c, c->d_idx, c->L, 0, c->L, (const double*)c->d_y, nullptr, (double*)dst->d_y, B)
+           : launch_colsum<float>(c, c->d_idx, c->L, 0, c->L, (const float*)c->d_y, nullptr, (float*)dst->d_y, B);
+  if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }

@@ -58,6 +58,15 @@ def make_ordering(L: int, M: int, n: int, seed: int = 0) -> np.ndarray:
     exactly as in the reference; memoised because every Monte-Carlo rep of
     the reference rebuilds the same seed-0 table (sparc_ldpc.py:433).
     """
+    if seed is None:  # RandomState(None): a fresh design from OS entropy, never memoised
+        w = _w_of(n, M)
+        rng = np.random.RandomState(None)
+        ordering = np.empty((L, n), dtype=np.uint32)
+        idxs = np.arange(1, w, dtype=np.uint32)
+        for ll in range(L):
+            rng.shuffle(idxs)
+            ordering[ll] = idxs[:n]
+        return ordering
     key = (int(L), int(M), int(n), int(seed))
     hit = _ORDER_CACHE.get(key)
     if hit is not None:
@@ -272,6 +281,23 @@ class SparcOperator:
                                        None if dst is None else dst.ctx,
                                        idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
         return idx
+
+    def threshold(self, B, l0, ns, app, threshold):
+        """Threshold decisions of sections [l0, l0+ns) from LLRs ``app`` -> (B, ns) int32, -1 undecided."""
+        if not isinstance(app, int):
+            app = as_f64(app)
+        p, fl = self._ptr(app)
+        idx = np.empty((B, ns), dtype=np.int32)
+        check(self._lib.sa_threshold(self._ctx, int(B), int(l0), int(ns), p, fl, float(threshold),
+                                     idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
+        return idx
+
+    def cancel(self, idx, dst):
+        """Stage y - A β(idx) (idx (B, L), -1 = keep) as dst's input y."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        assert idx.ndim == 2 and idx.shape[1] == self.L
+        check(self._lib.sa_cancel(self._ctx, idx.shape[0], idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32)),
+                                  dst.ctx))
 
     def subset(self, sections) -> "SparcOperator":
         """Operator over the given parent sections (sparc_transforms_shorter)."""

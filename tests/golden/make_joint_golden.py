@@ -117,6 +117,61 @@ def main():
                     out[key + f"|app{k}"] = app
                     out[key + f"|it{k}"] = np.array([it])
                 print(key, np.round(res, 5), [c[2] for c in calls], f"{time.time() - t0:.1f}s", flush=True)
+    # amp_exit.py does `from sparc_ldpc import *` while sparc_ldpc imports amp_exit:
+    # imported as a module (not run as a script) amp_exit sees a half-initialised
+    # sparc_ldpc.  Give it the names a script run would have bound.
+    ae = ref.ae
+    for name in dir(ref):
+        if not name.startswith("_") and not hasattr(ae, name):
+            setattr(ae, name, getattr(ref, name))
+    ae.amp = amp_np2
+
+    # ---- threshold-initialised exchange (sparc_ldpc.py:862-1047) -------------------
+    for tag, L, M, P, r, T, z, sigma, seeds, thr in (("thr", 64, 16, 4.0, 1.0, 30, 8, 0.93, (1, 2, 3, 4, 5, 6, 7, 8), 0.7),):
+        sp = ref.SPARCParams(L, M, sigma, P, r, T)
+        lp = ref.LDPCParams("802.16", "5/6", z)
+        out[f"{tag}|cfg"] = np.array([L, M, P, r, T, z, sigma, thr])
+        for s in seeds:
+            calls.clear()
+            first_idx.clear()
+            np.random.seed(s)
+            ba, bl, R = ref.soft_amp_ldpc_hardinit(sp, lp, 3, thr)
+            key = f"{tag}|hardinit|{s}"
+            out[key + "|ber"] = np.array(list(ba) + list(bl))
+            out[key + "|R"] = np.array([R])
+            out[key + "|idx"] = first_idx[0]
+            for k, (ch, app, it) in enumerate(calls):
+                out[key + f"|llr{k}"] = ch
+                out[key + f"|app{k}"] = app
+                out[key + f"|it{k}"] = np.array([it])
+            print(key, np.round(list(ba) + list(bl), 5), [c[2] for c in calls], flush=True)
+
+    # ---- EXIT: calc_E (amp_exit.py:185-270) ------------------------------------------
+    _spo = np.set_printoptions
+
+    def _spo_np2(*a, **k):  # amp_exit.py:261 passes threshold=np.nan, rejected by NumPy 2
+        if k.get("threshold", 0) != k.get("threshold", 0):
+            k["threshold"] = sys.maxsize
+        return _spo(*a, **k)
+
+    np.set_printoptions = _spo_np2
+    L, M, P, r, T = 64, 16, 4.0, 1.0, 30
+    sp = ref.SPARCParams(L, M, None, P, r, T)
+    out["exit|cfg"] = np.array([L, M, P, r, T])
+    for s, (I_a, snr_db, thr) in enumerate(((0.3, 12.0, 0.5), (0.6, 11.0, 0.7), (0.8, 10.0, 0.5), (0.95, 13.0, 0.9))):
+        np.random.seed(100 + s)
+        X = ae.gen_bits(int(L * np.log2(M)))
+        E = ae.calc_E(X, I_a, snr_db, sp, None, thr)
+        key = f"exit|{s}"
+        out[key + "|X"] = X
+        out[key + "|E"] = E
+        out[key + "|par"] = np.array([I_a, snr_db, thr])
+        PE_pos, PE_neg, mp, mn, vp, vn, bw = ae.hist_E(X, E)
+        out[key + "|hist"] = np.array([mp, mn, vp, vn, bw, ae.calc_I_e(PE_pos, PE_neg, bw)])
+        print(key, np.round(out[key + "|hist"], 4), flush=True)
+    np.set_printoptions = _spo
+    np.set_printoptions(threshold=1000)
+
     np.savez_compressed(os.path.join(HERE, "joint.npz"), **out)
 
 

@@ -1,0 +1,85 @@
+"""GPU: threshold-initialised exchange (soft_amp_ldpc_hardinit,
+sparc_ldpc.py:862-1047) and the AMP EXIT measurement calc_E (amp_exit.py:185-270)
+against reps of the reference itself (tests/golden/joint.npz, seeded np.random,
+fp64).  BERs exactly when the reference's BP calls converged, else within
+0.03; extrinsic LLRs E within 1e-8 relative where |E| < 50 (the clip at +-55
+and saturated values compared by sign), histogram statistics within 1e-6."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _keys(prefix):
+    g = golden("joint.npz")
+    depth = prefix.count("|") + 1  # key fields + the array name
+    return sorted({k.rsplit("|", 1)[0] for k in g
+                   if k.startswith(prefix) and k.count("|") == depth and not k.endswith("|cfg")})
+
+
+@pytest.mark.parametrize("key", _keys("thr|hardinit|"))
+def test_hardinit_reps_match_reference(key):
+    import sparc_ldpc_amd as sp
+    g = golden("joint.npz")
+    L, M, P, r, T, z, sigma, thr = g["thr|cfg"]
+    spp = sp.SPARCParams(int(L), int(M), float(sigma), float(P), float(r), int(T))
+    lp = sp.LDPCParams("802.16", "5/6", int(z))
+    np.random.seed(int(key.split("|")[-1]))
+    ba, bl, R = sp.soft_amp_ldpc_hardinit(spp, lp, 3, float(thr))
+    got = np.array(list(ba) + list(bl))
+    ref = g[key + "|ber"]
+    assert got.shape == ref.shape and abs(R - g[key + "|R"][0]) < 1e-15
+    assert got[0] == ref[0]
+    its = [int(g[key + f"|it{k}"][0]) for k in range(3) if key + f"|it{k}" in g]
+    if all(i < 200 for i in its):
+        np.testing.assert_array_equal(got, ref)
+    else:
+        assert np.max(np.abs(got - ref)) <= 0.03
+
+
+@pytest.mark.parametrize("key", _keys("exit|"))
+def test_calc_E_matches_reference(key):
+    import sparc_ldpc_amd as sp
+    g = golden("joint.npz")
+    L, M, P, r, T = g["exit|cfg"]
+    spp = sp.SPARCParams(int(L), int(M), None, float(P), float(r), int(T))
+    I_a, snr_db, thr = g[key + "|par"]
+    s = int(key.split("|")[1])
+    np.random.seed(100 + s)
+    X = sp.threshold.gen_bits(int(L * np.log2(M)))
+    assert np.array_equal(X, g[key + "|X"])
+    E = sp.calc_E(X, float(I_a), float(snr_db), spp, None, float(thr))
+    Er = g[key + "|E"]
+    mid = np.abs(Er) < 50
+    np.testing.assert_allclose(E[mid], Er[mid], rtol=1e-8, atol=1e-8)
+    assert np.array_equal(np.sign(E[~mid]), np.sign(Er[~mid]))
+    h = sp.hist_E(X, E)
+    got = np.array([h[2], h[3], h[4], h[5], h[6], sp.calc_I_e(h[0], h[1], h[6])])
+    np.testing.assert_allclose(got, g[key + "|hist"], rtol=1e-6, atol=1e-9)
+
+
+def test_hard_initialisation_dropin():
+    """amp_exit.hard_initialisation with the reference's signature: decided
+    sections cancelled through the device Ab, the rest on a shortened operator."""
+    import sparc_ldpc_amd as sp
+    L, M, n = 32, 16, 128
+    Ab, Az, ordering = sp.sparc_transforms(L, M, n, precision="fp64")
+    Pl = 4.0 / L * np.ones(L)
+    rs = np.random.RandomState(3)
+    beta = rs.dirichlet(np.ones(M) * 0.05, L).reshape(-1, 1)
+    y = rs.randn(n, 1)
+    b = beta.copy()
+    y_new, Ab_new, Az_new, secs, Ls = sp.hard_initialisation(b, L, M, n, ordering, y, Pl, Ab, 0.6, 20)
+    # decided = LDPC sections (last 20) with exactly one entry > 0.6
+    dec = [l for l in range(L - 20, L) if (beta[l * M:(l + 1) * M, 0] > 0.6).sum() == 1]
+    assert secs == [l for l in range(L) if l not in dec] and Ls == len(secs)
+    ref = np.zeros((L * M, 1))
+    for l in dec:
+        ref[l * M + int(np.argmax(beta[l * M:(l + 1) * M, 0]))] = np.sqrt(n * Pl[l])
+    assert np.array_equal(b, ref)
+    np.testing.assert_allclose(y_new, y - Ab(ref), rtol=0, atol=1e-12)
+    v = rs.randn(Ls * M, 1)
+    Ab_s, _ = sp.sparc_transforms_shorter(Ls, M, n, ordering[secs], precision="fp64")
+    np.testing.assert_allclose(Ab_new(v), Ab_s(v), rtol=0, atol=1e-12)

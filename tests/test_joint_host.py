@@ -8,7 +8,8 @@ from conftest import golden
 
 
 def _cases(g):
-    keys = sorted({k.rsplit("|", 1)[0] for k in g if k.count("|") == 3})
+    keys = sorted({k.rsplit("|", 1)[0] for k in g if k.count("|") == 3
+                   and k.split("|")[1] in ("originalHard", "soft", "hard")})
     for key in keys:
         tag, mode, seed = key.split("|")
         yield key, tag, mode, int(seed)

@@ -207,6 +207,16 @@ __device__ __forceinline__ real wave_sum_parts(const real* p, int cnt) {
   return wave_sum(s);
 }
 
+// The same sum for cnt <= 128 partials already loaded by the caller (lane i
+// holds partials i and i + 64, zero beyond cnt).
+template <typename real>
+__device__ __forceinline__ real wave_sum_pair(real a, real b) {
+  real s = 0;
+  s += a;
+  s += b;
+  return wave_sum(s);
+}
+
 // tau_t from the row kernel's per-block partial sums of z^2: sparc_ldpc.py:203.
 template <typename real>
 __device__ __forceinline__ real tau_from_parts(const real* zzp, int NZ, int n) {
@@ -401,7 +411,19 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
   constexpr int KH = E >= 16 ? 2 : (E >= 8 ? 16 : 16);
   constexpr int NQ = (E + 3) / 4;
   constexpr int KR = 8;  // rows per thread whose Ab-table loads are in flight together
-  const int g = blockIdx.x / a.RS, rsi = blockIdx.x % a.RS, b = blockIdx.y;
+  // The RS workgroups of a section group read the same bucket tables and
+  // previous estimate: place them on one XCD (workgroup j runs on XCD j % 8)
+  // so the second reader is served by that XCD's L2.
+  int g, rsi;
+  if (a.RS > 1 && (a.G & 7) == 0) {
+    const int j = blockIdx.x, u = j >> 3;
+    rsi = u % a.RS;
+    g = (u / a.RS) * 8 + (j & 7);
+  } else {
+    g = blockIdx.x / a.RS;
+    rsi = blockIdx.x % a.RS;
+  }
+  const int b = blockIdx.y;
   const int rows_per = (a.n + a.RS - 1) / a.RS;
   const int rb0 = rsi * rows_per, rb1 = min(a.n, rb0 + rows_per);
   const bool owner = rsi == 0;  // writes beta / beta^2 / tau for the group
@@ -968,6 +990,20 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
     if (a.early_stop && tau == last) return;
     tau2 = tau * tau;
   }
+  // wave 0 finishes the rows: its operands that do not depend on the Ab
+  // partials (y, z, the beta^2 partials) are loaded up front, in the same
+  // round trip as the partials
+  const size_t o = (size_t)b * n + (r < n ? r : 0);
+  real yv = 0, zv = 0, bbv[2] = {0, 0};
+  if (wv == 0) {
+    yv = a.y[o];
+    if (a.mode == ROW_AMP) {
+      zv = a.z[o];
+      const real* bp = a.bbp + (size_t)b * a.Gb;
+      bbv[0] = lane < a.Gb ? bp[lane] : (real)0;
+      bbv[1] = lane + 64 < a.Gb ? bp[lane + 64] : (real)0;
+    }
+  }
   if (a.mode != ROW_INIT0) {
     const int gq = (a.G + kRowWaves - 1) / kRowWaves;
     const int g0 = wv * gq, g1 = min(a.G, g0 + gq);
@@ -988,14 +1024,13 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   if (wv != 0) return;
   real ons = 0;
   if (a.mode == ROW_AMP) {
-    const real bb = wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
+    const real bb = a.Gb <= 128 ? wave_sum_pair(bbv[0], bbv[1]) : wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
     ons = a.P - bb / (real)n;
   }
   real zn = 0;
   if (r < n) {
-    const size_t o = (size_t)b * n + r;
     if (a.mode == ROW_INIT0) {
-      zn = a.y[o];
+      zn = yv;
     } else {
       real acc = 0;
       for (int w = 0; w < kRowWaves; ++w) acc += red[w][lane];
@@ -1004,8 +1039,8 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
         a.out[o] = ab;
         return;
       }
-      zn = a.y[o] - ab;
-      if (a.mode == ROW_AMP) zn += (a.z[o] / tau2) * ons;
+      zn = yv - ab;
+      if (a.mode == ROW_AMP) zn += (zv / tau2) * ons;
     }
     a.z[o] = zn;
   }

@@ -336,6 +336,43 @@ struct SecArgs {
 // Bucket-table loads of KH consecutive h-steps for one wave's section:
 // tb[hh][j] = inv[h*M + e0(j) .. +Q) (lanes >= M of a small-M section read
 // column 0; their values are discarded).
+// Staging z (n values) into LDS with 16-B loads: all kZU loads per thread
+// are issued up front (static register indices: no scratch), stored after the
+// round trip; n beyond 256*kZU 16-B vectors falls back to a plain loop.
+constexpr int kZU = 10;
+// (explicit members rather than an array: the array form was not promoted to
+// registers and its spill store waited for the loads at kernel start)
+#define SA_ZU_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9)
+using d2v = double __attribute__((ext_vector_type(2)));
+template <typename real>
+struct ZStage {
+  // native vector types: HIP's float4 (a struct of unions) defeats SROA
+  using vec_t = typename std::conditional<sizeof(real) == 4, f4, d2v>::type;
+  static constexpr int V = 16 / sizeof(real);
+#define SA_ZU_DECL(u) vec_t t##u;
+  SA_ZU_EACH(SA_ZU_DECL)
+#undef SA_ZU_DECL
+  int nv;
+  __device__ __forceinline__ void issue(const real* zb, int n, int tid) {
+    nv = ((reinterpret_cast<uintptr_t>(zb) & 15) == 0) ? n / V : 0;
+    const vec_t* zv = reinterpret_cast<const vec_t*>(zb);
+    const int last = nv > 0 ? nv - 1 : 0;
+#define SA_ZU_LOAD(u) { const int j = u * 256 + tid; t##u = zv[j < nv ? j : last]; }
+    if (nv > 0) { SA_ZU_EACH(SA_ZU_LOAD) }
+#undef SA_ZU_LOAD
+  }
+  __device__ __forceinline__ void store(real* zs, const real* zb, int n, int tid) const {
+    vec_t* zsv = reinterpret_cast<vec_t*>(zs);
+    const vec_t* zv = reinterpret_cast<const vec_t*>(zb);
+#define SA_ZU_STORE(u) { const int j = u * 256 + tid; if (j < nv) zsv[j] = t##u; }
+    SA_ZU_EACH(SA_ZU_STORE)
+#undef SA_ZU_STORE
+    for (int j = kZU * 256 + tid; j < nv; j += 256) zsv[j] = zv[j];
+    for (int i = nv * V + tid; i < n; i += 256) zs[i] = zb[i];
+    if (tid == 0) zs[n] = 0;
+  }
+};
+
 template <int E, int KH>
 __device__ __forceinline__ void load_buckets(const uint16_t* __restrict__ il, int h0, int nhi, int M,
                                              int lane, ushort4 (&tb)[KH][(E + 3) / 4]) {
@@ -465,16 +502,8 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     // bucket-table chunk, the previous beta, c_l, the first Ab-table rows and
     // the z^2 partials for tau.
     const real* zb = a.z + (size_t)b * n;
-    constexpr int V = 16 / sizeof(real);
-    using vec_t = typename std::conditional<sizeof(real) == 4, float4, double2>::type;
-    const bool aligned = ((reinterpret_cast<uintptr_t>(zb) & 15) == 0);
-    const int nv = aligned ? n / V : 0;
-    const int nfull = nv / (256 * 4) * (256 * 4);
-    vec_t t4[4];
-    if (nfull > 0) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) t4[u] = reinterpret_cast<const vec_t*>(zb)[u * 256 + tid];
-    }
+    ZStage<real> zst;
+    zst.issue(zb, n, tid);
     load_buckets<E, KH>(il, 0, a.nhi, M, lane, tb);
     if (a.mode == SEC_AMP) load_section<real, E>(bl, bprev, lane, M);
     const real cl = a.c[lc];
@@ -498,16 +527,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
       tau2 = tau * tau;
     }
     STAMP(1);
-    for (int i0 = 0; i0 < nfull; i0 += 256 * 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) reinterpret_cast<vec_t*>(zs)[i0 + u * 256 + tid] = t4[u];
-      if (i0 + 256 * 4 < nfull) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) t4[u] = reinterpret_cast<const vec_t*>(zb)[i0 + 256 * 4 + u * 256 + tid];
-      }
-    }
-    for (int i = nfull * V + tid; i < n; i += 256) zs[i] = zb[i];
-    if (tid == 0) zs[n] = 0;
+    zst.store(zs, zb, n, tid);
     __syncthreads();
   STAMP(2);
 
@@ -606,6 +626,194 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
 #endif
 }
 
+
+// ---------------------------------------------------------------------------
+// Single-codeword section kernel, two wavefronts per section (M >= 128)
+// ---------------------------------------------------------------------------
+// One workgroup = 2 sections x 2 wavefronts; wave w of a section holds the
+// half of its M entries whose top index bit is w (E2 = M/128 per lane, the
+// k_sec element layout within the half).  Compared with k_sec (one wave per
+// section, 4 sections per workgroup, the rows split over RS duplicated
+// workgroups) every CU gathers half as many LDS words and loads a third less
+// table data, and no workgroup repeats another's section work.  The top-bit
+// FWHT stage and the section max / sums cross the two waves through LDS.
+// Ab partials: G2 = ceil(L/2) per codeword, each over all n rows.
+// FWHT stage on the top index bit, held by the two waves of a section:
+// (a, b) -> (a + b, a - b) through an LDS exchange (wave w = top bit).
+template <typename real, int E2>
+__device__ __forceinline__ void top_bit_stage(real (&v)[E2], real* mine, const real* other, int lane, int w) {
+#pragma unroll
+  for (int i = 0; i < E2; ++i) mine[i * 64 + lane] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < E2; ++i) {
+    const real p = other[i * 64 + lane];
+    v[i] = w ? p - v[i] : v[i] + p;
+  }
+  __syncthreads();
+}
+
+template <typename real, int E2>
+__global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
+  STAMP(0);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int KH = E2 >= 16 ? 2 : 16;
+  constexpr int NQ = (E2 + 3) / 4;
+  // every row's Ab-table entry is loaded at kernel start (KR per thread covers
+  // n <= 256 * KR in one pass; larger n loops over further passes)
+  constexpr int KR = 18;
+  const int g = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int sidx = wv >> 1, w = wv & 1;
+  const int M = a.M, n = a.n, Mh = M >> 1;
+  const size_t LM = (size_t)a.L * M;
+  const int l = g * 2 + sidx;
+  const bool have = l < a.L;
+  const int lc = have ? l : a.L - 1;
+  const int eoff = w * Mh;
+
+  real* zs = reinterpret_cast<real*>(smem);
+  const int zslots = ((n + 1) * (int)sizeof(real) + 15) / 16 * 16 / (int)sizeof(real);
+  real* ts = zs + zslots;        // [2][M]   T_l = H_M beta_l
+  real* xb = ts + 2 * M;         // [4][E2*64] top-bit exchange
+  real* red = xb + 4 * E2 * 64;  // [4][4]   per-wave max, S, S2, beta^2
+
+  real v[E2];
+  real bprev[E2];
+  const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
+  real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
+  const uint16_t* il = a.inv + (size_t)lc * a.w + eoff;
+  // (k | sign << 15) of this pair's two sections for row r: one 4-B half of the
+  // 4-section entry of the fwd table
+  const uint32_t* fw = reinterpret_cast<const uint32_t*>(a.fwd) + (size_t)(g >> 1) * n * 2 + (g & 1);
+  ushort4 tb[KH][NQ];
+  uint32_t f[KR];
+
+  const real* zb = a.z + (size_t)b * n;
+  ZStage<real> zst;
+  zst.issue(zb, n, tid);
+  load_buckets<E2, KH>(il, 0, a.nhi, M, lane, tb);
+  load_section<real, E2>(bl, bprev, lane, Mh);
+  const real cl = a.c[lc];
+  const int nk = min(KR, (n + 255) / 256);  // passes of 256 rows in the first chunk
+#pragma unroll
+  for (int u = 0; u < KR; ++u) {
+    const int r = u * 256 + tid;
+    if (u < nk) f[u] = fw[(size_t)(r < n ? r : 0) * 2];
+  }
+  const real tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, n);
+  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+  const bool stop = a.early_stop && (tau == last);
+  if (g == 0 && tid == 0) {
+    a.tau[(size_t)b * a.T1 + a.t] = tau;
+    if (stop && a.iters[b] < 0) a.iters[b] = a.t;
+  }
+  if (stop) return;  // uniform over the grid row
+  const real tau2 = tau * tau;
+  STAMP(1);
+  zst.store(zs, zb, n, tid);
+  __syncthreads();
+  STAMP(2);
+
+  // bucket gather of z for this wave's half of the section
+#pragma unroll
+  for (int i = 0; i < E2; ++i) v[i] = 0;
+  for (int h0 = 0; h0 < a.nhi; h0 += KH) {
+    ushort4 tn[KH][NQ];
+    const bool more = h0 + KH < a.nhi;
+    if (more) load_buckets<E2, KH>(il, h0 + KH, a.nhi, M, lane, tn);
+    gather_buckets<real, E2, KH>(zs, h0, a.nhi, tb, v);
+    if (more) {
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh)
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) tb[hh][j] = tn[hh][j];
+    }
+  }
+  real* mine = xb + wv * (E2 * 64);
+  const real* other = xb + (wv ^ 1) * (E2 * 64);
+  STAMP(3);
+  fwht_wave<real, E2>(v, lane, 64);
+  top_bit_stage<real, E2>(v, mine, other, lane, w);
+  STAMP(4);
+
+  // denoiser (sparc_ldpc.py:213-219) over both halves of the section
+  const real inv_sn = (real)1 / a.sqrt_n;
+  const real kk = cl / tau2;
+  real mx = neg_inf<real>();
+#pragma unroll
+  for (int i = 0; i < E2; ++i) {
+    v[i] = fma(v[i], inv_sn, bprev[i]) * kk;
+    mx = v[i] > mx ? v[i] : mx;
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wv * 4] = mx;
+  __syncthreads();
+  const int w0 = wv & ~1;
+  mx = red[w0 * 4] > red[(w0 + 1) * 4] ? red[w0 * 4] : red[(w0 + 1) * 4];
+  real S = 0, S2 = 0;
+#pragma unroll
+  for (int i = 0; i < E2; ++i) {
+    v[i] = dexp<real>(v[i] - mx);
+    S += v[i];
+    S2 += v[i] * v[i];
+  }
+  wave_sum2(S, S2);
+  if (lane == 0) {
+    red[wv * 4 + 1] = S;
+    red[wv * 4 + 2] = S2;
+  }
+  __syncthreads();
+  S = red[w0 * 4 + 1] + red[(w0 + 1) * 4 + 1];
+  S2 = red[w0 * 4 + 2] + red[(w0 + 1) * 4 + 2];
+  const real scale = cl / S;
+#pragma unroll
+  for (int i = 0; i < E2; ++i) v[i] = have ? v[i] * scale : (real)0;
+  if (have) store_section<real, E2>(blo, v, lane, Mh);
+  const real bb = have ? S2 * scale * scale : (real)0;
+
+  STAMP(5);
+  fwht_wave<real, E2>(v, lane, 64);  // T_l = H_M beta_l
+  top_bit_stage<real, E2>(v, mine, other, lane, w);
+  STAMP(6);
+  {
+    real* tl = ts + sidx * M + eoff;
+#pragma unroll
+    for (int i = 0; i < E2; ++i) tl[elem_index<E2>(lane, i)] = v[i];
+  }
+  if (lane == 0) red[wv * 4 + 3] = bb;
+  __syncthreads();
+  STAMP(7);
+  if (tid == 0) a.bbp[(size_t)b * a.G + g] = red[0 * 4 + 3] + red[2 * 4 + 3];
+  // Ab partial of the pair for every row
+  real* abp = a.abp + ((size_t)b * a.G + g) * n;
+  for (int r0 = 0; r0 < n; r0 += 256 * KR) {
+    if (r0 > 0) {  // n > 256 * KR only
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        const int r = r0 + u * 256 + tid;
+        f[u] = fw[(size_t)(r < n ? r : 0) * 2];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      const int r = r0 + u * 256 + tid;
+      if (r < n) {
+        const uint32_t e = f[u];
+        const real v0 = ts[e & 0x7fffu];
+        const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
+        real t = (e & 0x8000u) ? -v0 : v0;
+        t += (e & 0x80000000u) ? -v1 : v1;
+        abp[r] = t;
+      }
+    }
+  }
+#ifdef SA_STAMPS
+  STAMP(8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(9);
+#endif
+}
 // ---------------------------------------------------------------------------
 // Batched section kernel (B codewords share the operator)
 // ---------------------------------------------------------------------------
@@ -1323,6 +1531,8 @@ struct sa_ctx {
   int RS = 1, KS = 1, Gd = 0;  // dense splits; Gd = dense denoiser groups
   size_t lda = 0;
   size_t sec_lds = 0;
+  int G2 = 0;          // k_sec2 pairs of sections (0: k_sec2 unavailable)
+  size_t sec2_lds = 0;
   std::vector<uint32_t> ordering;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1395,13 +1605,14 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   const size_t s = rsz(c), LM = (size_t)c->L * c->M;
   int Gmax = c->G > c->KS ? c->G : c->KS;
   if (c->Gb > Gmax) Gmax = c->Gb;
+  if (c->G2 > Gmax) Gmax = c->G2;
   int rc;
   if ((rc = dev_alloc(c, &c->d_y, nB * c->n * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_z, nB * c->n * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_beta, nB * LM * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_out, nB * (LM > (size_t)c->n ? LM : (size_t)c->n) * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_abp, (size_t)nB * Gmax * c->n * s))) return rc;
-  if ((rc = dev_alloc(c, &c->d_bbp, (size_t)nB * (c->G > c->Gd ? c->G : c->Gd) * s))) return rc;
+  if ((rc = dev_alloc(c, &c->d_bbp, (size_t)nB * Gmax * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZ * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_tau, (size_t)nB * (nT + 1) * s))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_iters, (size_t)nB * sizeof(int)))) return rc;
@@ -1417,7 +1628,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
     const size_t LMs = (size_t)c->L * c->M * s;
     void* bufs[] = {c->d_y, c->d_z, c->d_beta, c->d_out, c->d_abp, c->d_bbp, c->d_zzp, c->d_tau};
     const size_t sz[] = {nB * c->n * s, nB * c->n * s, nB * LMs, nB * (LMs > (size_t)c->n * s ? LMs : (size_t)c->n * s),
-                         (size_t)nB * Gmax * c->n * s, (size_t)nB * (c->G > c->Gd ? c->G : c->Gd) * s,
+                         (size_t)nB * Gmax * c->n * s, (size_t)nB * Gmax * s,
                          (size_t)nB * c->NZ * s, (size_t)nB * (nT + 1) * s};
     for (int i = 0; i < 8; ++i)
       if (mask & (1 << i)) HIP_TRY(hipMemsetAsync(bufs[i], 0xff, sz[i], c->stream));
@@ -1557,6 +1768,35 @@ int launch_secb(sa_ctx* c, int B, int t, int es) {
 
 bool use_batched(const sa_ctx* c, int B) { return c->CB > 0 && B >= 4; }
 
+// Two-waves-per-section kernel for the unbatched path when its G2 x B
+// workgroups fill at least half of the CUs (otherwise k_sec's row splits do).
+bool use_sec2(const sa_ctx* c, int B) {
+  return c->backend == SA_BACKEND_HADAMARD && !use_batched(c, B) && c->G2 > 0 && c->G2 * B * 2 >= c->n_cus &&
+         !getenv("SPARC_AMP_NO_SEC2");
+}
+
+template <typename real>
+int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout) {
+  SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
+  a.beta = (real*)bin;
+  a.beta_out = (real*)bout;
+  a.G = c->G2;
+  dim3 grid(c->G2, B);
+  if (c->prof) c->prof->begin(c->stream, K_SEC);
+  switch (c->M / 128) {
+    case 1: k_sec2<real, 1><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 2: k_sec2<real, 2><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 4: k_sec2<real, 4><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 8: k_sec2<real, 8><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 16: k_sec2<real, 16><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 32: k_sec2<real, 32><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    default: return fail(SA_ERR_UNSUPPORTED, "k_sec2: M");
+  }
+  if (c->prof) c->prof->end(c->stream);
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
 template <typename real>
 int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, void* bout = nullptr) {
   SecArgs<real> a = sec_args<real>(c, mode, t, es);
@@ -1688,9 +1928,10 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const int es = (flags & SA_FLAG_NO_EARLY_STOP) ? 0 : 1;
   const bool dense = c->backend == SA_BACKEND_DENSE;
   const bool batched = !dense && use_batched(c, B);
+  const bool sec2 = use_sec2(c, B);
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
-  const int G = dense ? c->KS : (batched ? c->Gb : c->G);
-  const int Gb = dense ? c->Gd : (batched ? c->Gb : c->G);
+  const int G = dense ? c->KS : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
+  const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
   int rc;
   k_fill32<<<(B + 255) / 256, 256, 0, c->stream>>>((uint32_t*)c->d_iters, 0xffffffffu, (size_t)B);
   if (has_b0) {
@@ -1716,7 +1957,11 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     } else {
       void* pin = (t & 1) ? c->d_beta2 : c->d_beta;
       void* pout = (t & 1) ? c->d_beta : c->d_beta2;
-      if ((rc = launch_sec<real>(c, B, SEC_AMP, t, es, pin, pout))) return rc;
+      if (sec2) {
+        if ((rc = launch_sec2<real>(c, B, t, es, pin, pout))) return rc;
+      } else if ((rc = launch_sec<real>(c, B, SEC_AMP, t, es, pin, pout))) {
+        return rc;
+      }
     }
     if ((rc = launch_row<real>(c, B, ROW_AMP, t, es, G, Gb))) return rc;
   }
@@ -1868,6 +2113,8 @@ hipError_t lds_attr_all() {
 #define SA_A(F) if (e == hipSuccess) e = hipFuncSetAttribute((const void*)F, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   SA_A((k_sec<real, 1>)) SA_A((k_sec<real, 2>)) SA_A((k_sec<real, 4>)) SA_A((k_sec<real, 8>))
   SA_A((k_sec<real, 16>)) SA_A((k_sec<real, 32>)) SA_A((k_sec<real, 64>))
+  SA_A((k_sec2<real, 1>)) SA_A((k_sec2<real, 2>)) SA_A((k_sec2<real, 4>)) SA_A((k_sec2<real, 8>))
+  SA_A((k_sec2<real, 16>)) SA_A((k_sec2<real, 32>))
   SA_A((k_secb<real, 1, 1, kWB>)) SA_A((k_secb<real, 2, 1, kWB>)) SA_A((k_secb<real, 4, 1, kWB>))
   SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
   SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
@@ -1940,6 +2187,13 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   }
   c->G = (L + kSpw - 1) / kSpw;
   c->Gb = (L + kWB - 1) / kWB;
+  if (M >= 128 && M <= 4096) {  // k_sec2: z + 2 sections' T + top-bit exchange + reductions
+    const size_t need = zbytes + 2 * (size_t)M * s + 4 * (size_t)(M / 2) * s + 16 * s;
+    if (need <= 160 * 1024) {
+      c->G2 = (L + 1) / 2;
+      c->sec2_lds = need;
+    }
+  }
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for
   // fp32 only) whose LDS image (z and T share one region) still lets two

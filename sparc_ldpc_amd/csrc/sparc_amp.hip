@@ -1257,6 +1257,93 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   if (lane == 0) a.zzp[(size_t)b * a.NZ + blockIdx.x] = s;
 }
 
+// Row kernel for small batches: 32 rows per 512-thread workgroup, so the
+// ceil(n/32) workgroups of a codeword spread over twice as many CUs as
+// k_row's 64-row workgroups.  Thread (row rl, group pg) sums the Ab
+// partials g = pg, pg+16, ... of its row in order
+// (all loads of a thread in flight together); the 16 group sums are added in
+// group order; wave 0 finishes the rows (Onsager residual, z^2 partial).
+constexpr int kRow2Rows = 32;  // one 128-B line of a partial per row block
+template <typename real>
+__global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
+  __shared__ real red[16][kRow2Rows + 1];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int rl = tid & (kRow2Rows - 1), pg = tid >> 5;
+  const int r = blockIdx.x * kRow2Rows + rl;
+  const int n = a.n;
+  real tau2 = 1;
+  if (a.mode == ROW_AMP) {
+    const real tau = a.tau[(size_t)b * a.T1 + a.t];
+    const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+    if (a.early_stop && tau == last) return;
+    tau2 = tau * tau;
+  }
+  const size_t o = (size_t)b * n + (r < n ? r : 0);
+  real yv = 0, zv = 0, bbv[4] = {0, 0, 0, 0};
+  if (tid < 64) {
+    yv = a.y[o];
+    if (a.mode == ROW_AMP) {
+      zv = a.z[o];
+      const real* bp = a.bbp + (size_t)b * a.Gb;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bbv[q] = tid + 64 * q < a.Gb ? bp[tid + 64 * q] : (real)0;
+    }
+  }
+  if (a.mode != ROW_INIT0) {
+    const real* p = a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
+    real acc = 0;
+    constexpr int U = 16;
+    for (int g0 = pg; g0 < a.G; g0 += 16 * U) {
+      real t[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int g = g0 + 16 * u;
+        t[u] = p[(size_t)(g < a.G ? g : pg) * n];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (g0 + 16 * u < a.G) acc += t[u];
+    }
+    red[pg][rl] = acc;
+  }
+  __syncthreads();
+  if (tid >= 64) return;
+  real ons = 0;
+  if (a.mode == ROW_AMP) {
+    real bb;
+    if (a.Gb <= 256) {
+      real sacc = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sacc += bbv[q];
+      bb = wave_sum(sacc);
+    } else {
+      bb = wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
+    }
+    ons = a.P - bb / (real)n;
+  }
+  real zn = 0;
+  if (tid < kRow2Rows && r < n) {
+    if (a.mode == ROW_INIT0) {
+      zn = yv;
+    } else {
+      real acc = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc += red[q][rl];
+      const real ab = acc / a.sqrt_n;
+      if (a.mode == ROW_ABOUT) {
+        a.out[o] = ab;
+        return;
+      }
+      zn = yv - ab;
+      if (a.mode == ROW_AMP) zn += (zv / tau2) * ons;
+    }
+    a.z[o] = zn;
+  }
+  if (a.mode == ROW_ABOUT) return;
+  const real sz = wave_sum(zn * zn);
+  if (tid == 0) a.zzp[(size_t)b * a.NZ + blockIdx.x] = sz;
+}
+
 // Per-section decision (sparc_ldpc.py:452-455): argmax, first index on ties.
 template <typename real, int E>
 __global__ void __launch_bounds__(256) k_decide(const real* beta, int32_t* idx, int L, int M) {
@@ -1532,6 +1619,8 @@ struct sa_ctx {
   size_t lda = 0;
   size_t sec_lds = 0;
   int G2 = 0;          // k_sec2 pairs of sections (0: k_sec2 unavailable)
+  int NZ16 = 0;        // k_row2 16-row blocks; nz_cur = z^2 partial count of the current decode
+  int nz_cur = 0;
   size_t sec2_lds = 0;
   std::vector<uint32_t> ordering;
   hipStream_t stream = nullptr;
@@ -1613,7 +1702,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   if ((rc = dev_alloc(c, &c->d_out, nB * (LM > (size_t)c->n ? LM : (size_t)c->n) * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_abp, (size_t)nB * Gmax * c->n * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_bbp, (size_t)nB * Gmax * s))) return rc;
-  if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZ * s))) return rc;
+  if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZ16 * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_tau, (size_t)nB * (nT + 1) * s))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_iters, (size_t)nB * sizeof(int)))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_idx, (size_t)nB * c->L * sizeof(int32_t)))) return rc;
@@ -1629,7 +1718,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
     void* bufs[] = {c->d_y, c->d_z, c->d_beta, c->d_out, c->d_abp, c->d_bbp, c->d_zzp, c->d_tau};
     const size_t sz[] = {nB * c->n * s, nB * c->n * s, nB * LMs, nB * (LMs > (size_t)c->n * s ? LMs : (size_t)c->n * s),
                          (size_t)nB * Gmax * c->n * s, (size_t)nB * Gmax * s,
-                         (size_t)nB * c->NZ * s, (size_t)nB * (nT + 1) * s};
+                         (size_t)nB * c->NZ16 * s, (size_t)nB * (nT + 1) * s};
     for (int i = 0; i < 8; ++i)
       if (mask & (1 << i)) HIP_TRY(hipMemsetAsync(bufs[i], 0xff, sz[i], c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1684,7 +1773,7 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
-  a.L = c->L; a.M = c->M; a.n = c->n; a.w = c->w; a.nhi = c->nhi; a.G = c->G; a.NZ = c->NZ;
+  a.L = c->L; a.M = c->M; a.n = c->n; a.w = c->w; a.nhi = c->nhi; a.G = c->G; a.NZ = c->nz_cur;
   a.T1 = c->Tcap + 1; a.t = t; a.mode = mode; a.early_stop = early_stop;
   a.RS = 1;
   a.B = 0; a.NC = 0;
@@ -1698,7 +1787,7 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb
   a.y = (const real*)c->d_y; a.z = (real*)c->d_z; a.abp = (const real*)c->d_abp;
   a.bbp = (const real*)c->d_bbp; a.zzp = (real*)c->d_zzp; a.tau = (const real*)c->d_tau;
   a.out = (real*)c->d_out;
-  a.n = c->n; a.G = G; a.NZ = c->NZ;
+  a.n = c->n; a.G = G; a.NZ = c->nz_cur;
   a.Gb = Gb; a.T1 = c->Tcap + 1; a.t = t; a.mode = mode;
   a.early_stop = early_stop;
   // the dense matrix already carries the 1/sqrt(n) of sparc_ldpc.py:143-146
@@ -1819,14 +1908,13 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
 template <typename real>
 int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb) {
   RowArgs<real> a = row_args<real>(c, mode, t, es, G, Gb);
-  dim3 grid(c->NZ, B);
   if (c->prof) c->prof->begin(c->stream, K_ROW);
-  // few blocks (small batch): 16 waves split the partials; many blocks: 4
-  // waves with deeper per-lane load streams
-  if (B * c->NZ < 4 * c->n_cus)
-    k_row<real, 16><<<grid, 16 * 64, 0, c->stream>>>(a);
+  // small batch: 16-row workgroups cover the chip; many codewords: 64-row
+  // workgroups, 4 waves with deeper per-lane load streams
+  if (c->nz_cur == c->NZ16)
+    k_row2<real><<<dim3(c->NZ16, B), 16 * kRow2Rows, 0, c->stream>>>(a);
   else
-    k_row<real, 4><<<grid, 4 * 64, 0, c->stream>>>(a);
+    k_row<real, 4><<<dim3(c->NZ, B), 4 * 64, 0, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -1837,7 +1925,7 @@ DenseArgs dense_args(sa_ctx* c, int t, int es, int mode) {
   a.A = c->d_A; a.z = (const float*)c->d_z; a.azp = (float*)c->d_azp;
   a.beta = (const float*)c->d_beta; a.abp = (float*)c->d_abp; a.zzp = (const float*)c->d_zzp;
   a.tau = (const float*)c->d_tau;
-  a.L = c->L; a.M = c->M; a.n = c->n; a.NZ = c->NZ; a.T1 = c->Tcap + 1; a.t = t;
+  a.L = c->L; a.M = c->M; a.n = c->n; a.NZ = c->nz_cur; a.T1 = c->Tcap + 1; a.t = t;
   a.early_stop = es; a.RS = c->RS; a.KS = c->KS; a.mode = mode; a.lda = c->lda;
   return a;
 }
@@ -1929,6 +2017,7 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const bool dense = c->backend == SA_BACKEND_DENSE;
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
+  c->nz_cur = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;  // z^2 partials: k_row2 or k_row blocks
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
   const int G = dense ? c->KS : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
   const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
@@ -2177,6 +2266,8 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   c->E = M >= 64 ? M / 64 : 1;
   c->ordering.assign(ordering, ordering + (size_t)L * n);
   c->NZ = (n + kRowsPerBlk - 1) / kRowsPerBlk;
+  c->NZ16 = (n + kRow2Rows - 1) / kRow2Rows;
+  c->nz_cur = c->NZ;
   // section kernel LDS: z slots + 4 sections x M + 4 beta^2 partials
   const size_t s = rsz(c);
   const size_t zbytes = ((size_t)(n + 1) * s + 15) / 16 * 16;

@@ -217,6 +217,31 @@ __device__ __forceinline__ real wave_sum_pair(real a, real b) {
   return wave_sum(s);
 }
 
+// The z^2 partials for tau, loaded ahead of everything else a kernel needs
+// (vmcnt retires loads in order: tau then waits for these alone).  Same sum
+// as wave_sum_parts for NZ <= 64 * kZZ.
+constexpr int kZZ = 4;
+template <typename real>
+struct ZZParts {
+  real v[kZZ];
+  __device__ __forceinline__ void issue(const real* p, int cnt, int lane) {
+#pragma unroll
+    for (int q = 0; q < kZZ; ++q) v[q] = lane + 64 * q < cnt ? p[lane + 64 * q] : (real)0;
+  }
+  __device__ __forceinline__ real tau(const real* p, int cnt, int n) const {
+    real s;
+    if (cnt <= 64 * kZZ) {
+      s = 0;
+#pragma unroll
+      for (int q = 0; q < kZZ; ++q) s += v[q];
+      s = wave_sum(s);
+    } else {
+      s = wave_sum_parts(p, cnt);
+    }
+    return dsqrt<real>(s / (real)n);
+  }
+};
+
 // tau_t from the row kernel's per-block partial sums of z^2: sparc_ldpc.py:203.
 template <typename real>
 __device__ __forceinline__ real tau_from_parts(const real* zzp, int NZ, int n) {
@@ -689,6 +714,11 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
   ushort4 tb[KH][NQ];
   uint32_t f[KR];
 
+  // loads in the order they are needed (vmcnt retires them in order)
+  const real* zzb = a.zzp + (size_t)b * a.NZ;
+  ZZParts<real> zz;
+  zz.issue(zzb, a.NZ, lane);
+  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
   const real* zb = a.z + (size_t)b * n;
   ZStage<real> zst;
   zst.issue(zb, n, tid);
@@ -701,8 +731,7 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
     const int r = u * 256 + tid;
     if (u < nk) f[u] = fw[(size_t)(r < n ? r : 0) * 2];
   }
-  const real tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, n);
-  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+  const real tau = zz.tau(zzb, a.NZ, n);
   const bool stop = a.early_stop && (tau == last);
   if (g == 0 && tid == 0) {
     a.tau[(size_t)b * a.T1 + a.t] = tau;

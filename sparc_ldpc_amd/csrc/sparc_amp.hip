@@ -1005,11 +1005,15 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
   const uint16_t* il = a.inv + (size_t)lc * a.w;
   ushort4 tb[KH][NQ];
   load_buckets<E, KH>(il, 0, a.nhi, M, lane, tb);
-  real bprev[PB ? CB : 1][E];
+  // previous beta: all CB codewords up front when registers allow (CB <= 2),
+  // else codeword 0 now and codeword c+1 while c is denoised (PB false)
+  real bprev[PB ? CB : 2][E];
   if constexpr (PB) {
 #pragma unroll
     for (int c = 0; c < CB; ++c)
       load_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lane, M);
+  } else {
+    load_section<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lane, M);
   }
   const real cl = a.c[lc];
   const ushort4* fw = a.fwd + (size_t)g * W4 * n;
@@ -1104,10 +1108,13 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
   real bbl[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
+    if constexpr (!PB) {
+      if (c + 1 < CB)
+        load_section<real, E>(a.beta + (size_t)bc[c + 1] * LM + (size_t)lc * M, bprev[(c + 1) & 1], lane, M);
+    }
     fwht_wave<real, E>(v[c], lane, mlanes);
     real* bl = a.beta + (size_t)bc[c] * LM + (size_t)lc * M;
-    if constexpr (!PB) load_section<real, E>(bl, bprev[0], lane, M);
-    bbl[c] = denoise_section<real, E>(v[c], bprev[PB ? c : 0], bl, lane, M, cl, tau2[c], a.sqrt_n,
+    bbl[c] = denoise_section<real, E>(v[c], bprev[PB ? c : (c & 1)], bl, lane, M, cl, tau2[c], a.sqrt_n,
                                       have && live[c]);
     if (have) {
       fwht_wave<real, E>(v[c], lane, mlanes);  // T_l = H_M beta_l

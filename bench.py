@@ -205,8 +205,9 @@ def main():
     # library's stream), for the roofline of the dominant kernel
     kinds, total_ms = op.profile(B, T, early_stop=False)
     s = 8 if args.precision == "fp64" else 4
+    plan = op.plan(B)
     if args.backend == "hadamard":
-        G = (L + 3) // 4
+        G = plan["partials"]  # Ab partials per codeword of the section kernel this batch runs
         wv = op.w
         per = {
             "k_sec": sec_bytes(L, M, n, wv, B, G, s),
@@ -219,9 +220,11 @@ def main():
     dom = max(share, key=share.get)
     dom_ms = kinds[dom][0]
     achieved = per[dom] / (dom_ms * 1e-3) / 1e9
-    pmc = load_pmc(f"{args.workload}_{args.backend}_{args.precision}_B{B}", dom)
+    pmc = load_pmc(f"{args.workload}_{args.backend}_{args.precision}_B{B}",
+                   {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom))
+    kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom)
     roofline = {
-        "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
         "algorithmic_bytes_per_launch": per[dom], "avg_launch_ms": round(dom_ms, 5),

@@ -156,6 +156,11 @@ int sa_threshold(sa_ctx* ctx, int B, int l0, int ns, const double* app, int flag
 int sa_cancel(sa_ctx* ctx, int B, const int32_t* idx, sa_ctx* dst);
 
 /* Introspection. */
+/* The kernels a decode of B codewords runs: out8 = {section kernel (0 k_sec,
+ * 1 k_sec2, 2 k_secb, 3 dense GEMVs), Ab partials per codeword, row splits,
+ * codewords per batched workgroup, z^2 partials, w, row kernel (1 k_row2,
+ * 0 k_row), 0}. */
+int sa_plan(sa_ctx* ctx, int B, int64_t* out8);
 int sa_info(const sa_ctx* ctx, int64_t* out8); /* L, M, n, w, backend, precision, device, bytes */
 int sa_device_count(void);
 const char* sa_last_error(void);

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("k_secb", "k_sec", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide"):
+    for k in ("k_secb", "k_sec2", "k_sec", "k_row2", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide"):
         if f"::{k}<" in name or f" {k}(" in name or f"::{k}(" in name:
             return k
     return name.split("(")[0][-40:]

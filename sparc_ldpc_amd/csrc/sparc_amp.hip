@@ -2967,6 +2967,22 @@ int sa_cancel(sa_ctx* c, int B, const int32_t* idx, sa_ctx* dst) {
   return SA_OK;
 }
 
+int sa_plan(sa_ctx* c, int B, int64_t* o) {
+  if (check_ctx(c) || !o || B <= 0) return fail(SA_ERR_ARG, "sa_plan: bad arguments");
+  const bool dense = c->backend == SA_BACKEND_DENSE;
+  const bool batched = !dense && use_batched(c, B);
+  const bool sec2 = use_sec2(c, B);
+  o[0] = dense ? 3 : (batched ? 2 : (sec2 ? 1 : 0));
+  o[1] = dense ? c->KS : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
+  o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
+  o[3] = batched ? c->CB : 1;
+  o[4] = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;
+  o[5] = c->w;
+  o[6] = B * c->NZ < 4 * c->n_cus ? 1 : 0;
+  o[7] = 0;
+  return SA_OK;
+}
+
 int sa_info(const sa_ctx* c, int64_t* o) {
   if (check_ctx(c) || !o) return fail(SA_ERR_ARG, "sa_info: bad arguments");
   o[0] = c->L; o[1] = c->M; o[2] = c->n; o[3] = c->w; o[4] = c->backend; o[5] = c->prec;

@@ -213,6 +213,16 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, dptr(out), iters.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return out, iters
 
+    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense")
+
+    def plan(self, B):
+        """Which kernels a decode of B codewords runs (sa_plan)."""
+        o = np.zeros(8, dtype=np.int64)
+        check(self._lib.sa_plan(self._ctx, int(B), o.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int64))))
+        return dict(section_kernel=self.SECTION_KERNELS[int(o[0])], partials=int(o[1]), row_splits=int(o[2]),
+                    codewords_per_wg=int(o[3]), zz_partials=int(o[4]), w=int(o[5]),
+                    row_kernel="k_row2" if o[6] else "k_row")
+
     def info(self):
         o = np.zeros(8, dtype=np.int64)
         check(self._lib.sa_info(self._ctx, o.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int64))))

@@ -4,6 +4,7 @@
 #   pass 2: --pmc FETCH_SIZE (own pass)   -> HBM read bytes per dispatch
 #   pass 3: --pmc WRITE_SIZE (own pass)   -> HBM write bytes per dispatch
 # Usage: bash scripts/profile.sh TAG [bench args...]
+#        SCRIPT=scripts/bench_joint.py bash scripts/profile.sh TAG [args...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-run}; shift
@@ -12,12 +13,15 @@ mkdir -p $OUT
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- \
-    python3 bench.py --no-cpu --no-dense "${BENCH_ARGS[@]}" > $OUT/$name.log 2>&1
+    python3 $SCRIPT "${EXTRA[@]}" "${BENCH_ARGS[@]}" > $OUT/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"
   return $rc
 }
 BENCH_ARGS=("$@")
+SCRIPT=${SCRIPT:-bench.py}
+EXTRA=(--no-cpu)
+[ "$SCRIPT" = bench.py ] && EXTRA+=(--no-dense)
 run trace --kernel-trace --stats && \
 run fetch --kernel-trace --pmc FETCH_SIZE && \
 run write --kernel-trace --pmc WRITE_SIZE

@@ -338,6 +338,7 @@ template <typename real>
 struct SecArgs {
   const uint16_t* __restrict__ inv;  // [L][w]  row of ordering value o, or n (zero slot)
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
+  const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
   const real* __restrict__ c;        // [L]     sqrt(n * Pl)
   const real* __restrict__ z;        // [B][n]
   real* __restrict__ beta;           // [B][L*M] previous estimate (read)
@@ -369,7 +370,7 @@ constexpr int kZU = 10;
 // registers and its spill store waited for the loads at kernel start)
 #define SA_ZU_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9)
 using d2v = double __attribute__((ext_vector_type(2)));
-template <typename real>
+template <typename real, int NT = 256>
 struct ZStage {
   // native vector types: HIP's float4 (a struct of unions) defeats SROA
   using vec_t = typename std::conditional<sizeof(real) == 4, f4, d2v>::type;
@@ -382,18 +383,18 @@ struct ZStage {
     nv = ((reinterpret_cast<uintptr_t>(zb) & 15) == 0) ? n / V : 0;
     const vec_t* zv = reinterpret_cast<const vec_t*>(zb);
     const int last = nv > 0 ? nv - 1 : 0;
-#define SA_ZU_LOAD(u) { const int j = u * 256 + tid; t##u = zv[j < nv ? j : last]; }
+#define SA_ZU_LOAD(u) if (u * NT < nv) { const int j = u * NT + tid; t##u = zv[j < nv ? j : last]; }
     if (nv > 0) { SA_ZU_EACH(SA_ZU_LOAD) }
 #undef SA_ZU_LOAD
   }
   __device__ __forceinline__ void store(real* zs, const real* zb, int n, int tid) const {
     vec_t* zsv = reinterpret_cast<vec_t*>(zs);
     const vec_t* zv = reinterpret_cast<const vec_t*>(zb);
-#define SA_ZU_STORE(u) { const int j = u * 256 + tid; if (j < nv) zsv[j] = t##u; }
+#define SA_ZU_STORE(u) { const int j = u * NT + tid; if (j < nv) zsv[j] = t##u; }
     SA_ZU_EACH(SA_ZU_STORE)
 #undef SA_ZU_STORE
-    for (int j = kZU * 256 + tid; j < nv; j += 256) zsv[j] = zv[j];
-    for (int i = nv * V + tid; i < n; i += 256) zs[i] = zb[i];
+    for (int j = kZU * NT + tid; j < nv; j += NT) zsv[j] = zv[j];
+    for (int i = nv * V + tid; i < n; i += NT) zs[i] = zb[i];
     if (tid == 0) zs[n] = 0;
   }
 };
@@ -708,9 +709,9 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
   const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
   real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
   const uint16_t* il = a.inv + (size_t)lc * a.w + eoff;
-  // (k | sign << 15) of this pair's two sections for row r: one 4-B half of the
-  // 4-section entry of the fwd table
-  const uint32_t* fw = reinterpret_cast<const uint32_t*>(a.fwd) + (size_t)(g >> 1) * n * 2 + (g & 1);
+  // (k | sign << 15) of this pair's two sections for row r (pair-major table:
+  // the workgroup reads only its own lines)
+  const uint32_t* fw = a.fwd2 + (size_t)g * n;
   ushort4 tb[KH][NQ];
   uint32_t f[KR];
 
@@ -729,7 +730,7 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
 #pragma unroll
   for (int u = 0; u < KR; ++u) {
     const int r = u * 256 + tid;
-    if (u < nk) f[u] = fw[(size_t)(r < n ? r : 0) * 2];
+    if (u < nk) f[u] = fw[r < n ? r : 0];
   }
   const real tau = zz.tau(zzb, a.NZ, n);
   const bool stop = a.early_stop && (tau == last);
@@ -821,12 +822,199 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
 #pragma unroll
       for (int u = 0; u < KR; ++u) {
         const int r = r0 + u * 256 + tid;
-        f[u] = fw[(size_t)(r < n ? r : 0) * 2];
+        f[u] = fw[r < n ? r : 0];
       }
     }
 #pragma unroll
     for (int u = 0; u < KR; ++u) {
       const int r = r0 + u * 256 + tid;
+      if (r < n) {
+        const uint32_t e = f[u];
+        const real v0 = ts[e & 0x7fffu];
+        const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
+        real t = (e & 0x8000u) ? -v0 : v0;
+        t += (e & 0x80000000u) ? -v1 : v1;
+        abp[r] = t;
+      }
+    }
+  }
+#ifdef SA_STAMPS
+  STAMP(8);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(9);
+#endif
+}
+// Four wavefronts per section (k_sec4): the k_sec2 workgroup of two sections
+// with 512 threads.  Wave q of a section holds quarter q (the two top index
+// bits); the two top FWHT stages cross the quarters in one LDS exchange with
+// the additions of two single-bit stages, ((x0 +- x1) +- (x2 +- x3)), so the
+// transform is bit-identical to k_sec2's.  Per wave the LDS gather chain and
+// the Ab row loop are half as long, and every SIMD runs two waves.
+template <typename real, int E4>
+__device__ __forceinline__ void top2_stage(real (&v)[E4], real* xs, int lane, int q) {
+  constexpr int QS = E4 * 64;  // one quarter
+#pragma unroll
+  for (int i = 0; i < E4; ++i) xs[q * QS + i * 64 + lane] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < E4; ++i) {
+    const real x0 = xs[i * 64 + lane], x1 = xs[QS + i * 64 + lane];
+    const real x2 = xs[2 * QS + i * 64 + lane], x3 = xs[3 * QS + i * 64 + lane];
+    const real lo = (q & 1) ? x0 - x1 : x0 + x1;
+    const real hi = (q & 1) ? x2 - x3 : x2 + x3;
+    v[i] = (q & 2) ? lo - hi : lo + hi;
+  }
+  __syncthreads();
+}
+
+template <typename real, int E4>
+__global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
+  STAMP(0);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NT = 512;
+  constexpr int KH = E4 >= 8 ? 4 : 16;
+  constexpr int NQ = (E4 + 3) / 4;
+  constexpr int KR = 9;  // rows per thread per pass: n <= 4608 in one pass
+  const int g = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int sidx = wv >> 2, q = wv & 3;
+  const int M = a.M, n = a.n, Mq = M >> 2;
+  const size_t LM = (size_t)a.L * M;
+  const int l = g * 2 + sidx;
+  const bool have = l < a.L;
+  const int lc = have ? l : a.L - 1;
+  const int eoff = q * Mq;
+
+  real* zs = reinterpret_cast<real*>(smem);
+  const int zslots = ((n + 1) * (int)sizeof(real) + 15) / 16 * 16 / (int)sizeof(real);
+  real* ts = zs + zslots;          // [2][M]   T_l = H_M beta_l
+  real* xb = ts + 2 * M;           // [2][M]   top-stage exchange, one M per section
+  real* red = xb + 2 * M;          // [8][4]   per-wave max, S, S2, beta^2
+
+  real v[E4];
+  real bprev[E4];
+  const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
+  real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
+  const uint16_t* il = a.inv + (size_t)lc * a.w + eoff;
+  const uint32_t* fw = a.fwd2 + (size_t)g * n;
+  ushort4 tb[KH][NQ];
+  uint32_t f[KR];
+
+  // loads in the order they are needed (vmcnt retires them in order)
+  const real* zzb = a.zzp + (size_t)b * a.NZ;
+  ZZParts<real> zz;
+  zz.issue(zzb, a.NZ, lane);
+  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+  const real* zb = a.z + (size_t)b * n;
+  ZStage<real, NT> zst;
+  zst.issue(zb, n, tid);
+  load_buckets<E4, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
+  load_section<real, E4>(bl, bprev, lane, Mq);
+  const real cl = a.c[lc];
+  const int nk = min(KR, (n + NT - 1) / NT);
+#pragma unroll
+  for (int u = 0; u < KR; ++u) {
+    const int r = u * NT + tid;
+    if (u < nk) f[u] = fw[r < n ? r : 0];
+  }
+  const real tau = zz.tau(zzb, a.NZ, n);
+  const bool stop = a.early_stop && (tau == last);
+  if (g == 0 && tid == 0) {
+    a.tau[(size_t)b * a.T1 + a.t] = tau;
+    if (stop && a.iters[b] < 0) a.iters[b] = a.t;
+  }
+  if (stop) return;  // uniform over the grid row
+  const real tau2 = tau * tau;
+  STAMP(1);
+  zst.store(zs, zb, n, tid);
+  __syncthreads();
+  STAMP(2);
+
+#pragma unroll
+  for (int i = 0; i < E4; ++i) v[i] = 0;
+  for (int h0 = 0; h0 < a.nhi; h0 += KH) {
+    ushort4 tn[KH][NQ];
+    const bool more = h0 + KH < a.nhi;
+    if (more) load_buckets<E4, KH>(il, h0 + KH, a.nhi, M, lane, tn);
+    gather_buckets<real, E4, KH>(zs, h0, a.nhi, tb, v);
+    if (more) {
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh)
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) tb[hh][j] = tn[hh][j];
+    }
+  }
+  real* xs = xb + sidx * M;
+  STAMP(3);
+  fwht_wave<real, E4>(v, lane, 64);
+  top2_stage<real, E4>(v, xs, lane, q);
+  STAMP(4);
+
+  // denoiser (sparc_ldpc.py:213-219) over the four quarters of the section
+  const real inv_sn = (real)1 / a.sqrt_n;
+  const real kk = cl / tau2;
+  real mx = neg_inf<real>();
+#pragma unroll
+  for (int i = 0; i < E4; ++i) {
+    v[i] = fma(v[i], inv_sn, bprev[i]) * kk;
+    mx = v[i] > mx ? v[i] : mx;
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wv * 4] = mx;
+  __syncthreads();
+  const int w0 = wv & ~3;
+  {
+    const real m01 = red[w0 * 4] > red[(w0 + 1) * 4] ? red[w0 * 4] : red[(w0 + 1) * 4];
+    const real m23 = red[(w0 + 2) * 4] > red[(w0 + 3) * 4] ? red[(w0 + 2) * 4] : red[(w0 + 3) * 4];
+    mx = m01 > m23 ? m01 : m23;
+  }
+  real S = 0, S2 = 0;
+#pragma unroll
+  for (int i = 0; i < E4; ++i) {
+    v[i] = dexp<real>(v[i] - mx);
+    S += v[i];
+    S2 += v[i] * v[i];
+  }
+  wave_sum2(S, S2);
+  if (lane == 0) {
+    red[wv * 4 + 1] = S;
+    red[wv * 4 + 2] = S2;
+  }
+  __syncthreads();
+  S = (red[w0 * 4 + 1] + red[(w0 + 1) * 4 + 1]) + (red[(w0 + 2) * 4 + 1] + red[(w0 + 3) * 4 + 1]);
+  S2 = (red[w0 * 4 + 2] + red[(w0 + 1) * 4 + 2]) + (red[(w0 + 2) * 4 + 2] + red[(w0 + 3) * 4 + 2]);
+  const real scale = cl / S;
+#pragma unroll
+  for (int i = 0; i < E4; ++i) v[i] = have ? v[i] * scale : (real)0;
+  if (have) store_section<real, E4>(blo, v, lane, Mq);
+  const real bb = have ? S2 * scale * scale : (real)0;
+
+  STAMP(5);
+  fwht_wave<real, E4>(v, lane, 64);  // T_l = H_M beta_l
+  top2_stage<real, E4>(v, xs, lane, q);
+  STAMP(6);
+  {
+    real* tl = ts + sidx * M + eoff;
+#pragma unroll
+    for (int i = 0; i < E4; ++i) tl[elem_index<E4>(lane, i)] = v[i];
+  }
+  if (lane == 0) red[wv * 4 + 3] = bb;
+  __syncthreads();
+  STAMP(7);
+  if (tid == 0) a.bbp[(size_t)b * a.G + g] = red[0 * 4 + 3] + red[4 * 4 + 3];
+  // Ab partial of the pair for every row
+  real* abp = a.abp + ((size_t)b * a.G + g) * n;
+  for (int r0 = 0; r0 < n; r0 += NT * KR) {
+    if (r0 > 0) {  // n > NT * KR only
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        const int r = r0 + u * NT + tid;
+        f[u] = fw[r < n ? r : 0];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      const int r = r0 + u * NT + tid;
       if (r < n) {
         const uint32_t e = f[u];
         const real v0 = ts[e & 0x7fffu];
@@ -1655,6 +1843,8 @@ struct sa_ctx {
   size_t lda = 0;
   size_t sec_lds = 0;
   int G2 = 0;          // k_sec2 pairs of sections (0: k_sec2 unavailable)
+  bool sec4 = false;   // k_sec4 (4 waves per section) fits and is chosen
+  size_t sec4_lds = 0;
   int NZ16 = 0;        // k_row2 16-row blocks; nz_cur = z^2 partial count of the current decode
   int nz_cur = 0;
   size_t sec2_lds = 0;
@@ -1663,6 +1853,7 @@ struct sa_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint16_t* d_inv = nullptr;
   uint16_t* d_fwd = nullptr;
+  uint32_t* d_fwd2 = nullptr;
   float* d_A = nullptr;
   // workspace
   int Bcap = 0, Tcap = 0;
@@ -1805,7 +1996,7 @@ int download(sa_ctx* c, double* dst, const void* src, size_t count) {
 template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
-  a.inv = c->d_inv; a.fwd = (const ushort4*)c->d_fwd; a.c = (const real*)c->d_c;
+  a.inv = c->d_inv; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.c = (const real*)c->d_c;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
@@ -1908,6 +2099,19 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout) {
   a.G = c->G2;
   dim3 grid(c->G2, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
+  if (c->sec4) {
+    switch (c->M / 256) {
+      case 1: k_sec4<real, 1><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 2: k_sec4<real, 2><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 4: k_sec4<real, 4><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 8: k_sec4<real, 8><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 16: k_sec4<real, 16><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      default: return fail(SA_ERR_UNSUPPORTED, "k_sec4: M");
+    }
+    if (c->prof) c->prof->end(c->stream);
+    HIP_TRY(hipGetLastError());
+    return SA_OK;
+  }
   switch (c->M / 128) {
     case 1: k_sec2<real, 1><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
     case 2: k_sec2<real, 2><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
@@ -2185,6 +2389,7 @@ int build_tables(sa_ctx* c) {
   std::vector<uint16_t> inv((size_t)L * w, (uint16_t)n);
   const int G = (L + kSG - 1) / kSG * (kSG / kSpw);  // padded to whole batched groups
   std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);  // [G][n][4]; missing sections -> (k 0, +)
+  std::vector<uint32_t> fwd2((size_t)((L + 1) / 2) * n, 0);  // [L/2][n] section pairs
   for (int l = 0; l < L; ++l) {
     const uint32_t* o = c->ordering.data() + (size_t)l * n;
     uint16_t* il = inv.data() + (size_t)l * w;
@@ -2197,18 +2402,21 @@ int build_tables(sa_ctx* c) {
         return fail(SA_ERR_ORDERING, "ordering row " + std::to_string(l) + " repeats value " + std::to_string(v));
       il[v] = (uint16_t)r;
       const uint32_t hi = v >> lgM;
-      fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)] =
-          (uint16_t)((v & (uint32_t)(M - 1)) | ((__builtin_popcount(hi) & 1u) << 15));
+      const uint16_t e = (uint16_t)((v & (uint32_t)(M - 1)) | ((__builtin_popcount(hi) & 1u) << 15));
+      fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)] = e;
+      fwd2[(size_t)(l / 2) * n + r] |= (uint32_t)e << (16 * (l & 1));
     }
   }
   int rc;
   if ((rc = dev_alloc(c, (void**)&c->d_inv, inv.size() * 2))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_fwd, fwd.size() * 2))) return rc;
+  if ((rc = dev_alloc(c, (void**)&c->d_fwd2, fwd2.size() * 4))) return rc;
   // On the context's (non-blocking) stream and waited for: a pageable
   // hipMemcpy may return once the data is staged, before the DMA lands, and
   // the null stream does not order the kernels of a non-blocking stream.
   HIP_TRY(hipMemcpyAsync(c->d_inv, inv.data(), inv.size() * 2, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_fwd, fwd.data(), fwd.size() * 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_fwd2, fwd2.data(), fwd2.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
@@ -2240,6 +2448,8 @@ hipError_t lds_attr_all() {
   SA_A((k_sec<real, 16>)) SA_A((k_sec<real, 32>)) SA_A((k_sec<real, 64>))
   SA_A((k_sec2<real, 1>)) SA_A((k_sec2<real, 2>)) SA_A((k_sec2<real, 4>)) SA_A((k_sec2<real, 8>))
   SA_A((k_sec2<real, 16>)) SA_A((k_sec2<real, 32>))
+  SA_A((k_sec4<real, 1>)) SA_A((k_sec4<real, 2>)) SA_A((k_sec4<real, 4>)) SA_A((k_sec4<real, 8>))
+  SA_A((k_sec4<real, 16>))
   SA_A((k_secb<real, 1, 1, kWB>)) SA_A((k_secb<real, 2, 1, kWB>)) SA_A((k_secb<real, 4, 1, kWB>))
   SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
   SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
@@ -2319,6 +2529,13 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     if (need <= 160 * 1024) {
       c->G2 = (L + 1) / 2;
       c->sec2_lds = need;
+    }
+    // k_sec4: z + 2 sections' T + one exchange image per section + reductions
+    const size_t need4 = zbytes + 4 * (size_t)M * s + 32 * s;
+    const char* e4 = getenv("SPARC_AMP_SEC4");
+    if (c->G2 > 0 && M >= 256 && need4 <= 160 * 1024 && !(e4 && e4[0] == '0')) {
+      c->sec4 = true;
+      c->sec4_lds = need4;
     }
   }
 
@@ -2426,63 +2643,78 @@ __global__ void __launch_bounds__(256) k_colsum(const ushort4* __restrict__ fwd,
   out[o] = base ? (real)((double)base[o] - x) : (real)(x + (add ? add[o] : 0.0));
 }
 
-// sp2bp + LLR (sparc_ldpc.py:470-479 -> :257-281): thread per (codeword,
-// section, bit).  p = sum over the entries j of the section whose bit
-// (logM-1-t) is set, ascending j, of beta_j / c_l (the reference's order);
-// llr = nan_to_num(log(1 - p) - log(p)).
-template <typename real>
-__global__ void k_llr(const real* __restrict__ beta, const double* __restrict__ cd, int L, int M, int lgM,
-                      int l0, int ns, int B, double* __restrict__ llr) {
-  const size_t tot = (size_t)B * ns * lgM;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
-    const int t = (int)(i % lgM);
-    const size_t bl = i / lgM;
-    const int lp = (int)(bl % ns), b = (int)(bl / ns), l = l0 + lp;
-    const int step = 1 << (lgM - 1 - t);
-    const real* bs = beta + ((size_t)b * L + l) * M;
-    const double c = cd[l];
-    double p = 0.0;
-    for (int k = step; k < M; k += 2 * step)
-      for (int j = k; j < k + step; ++j) p += (double)bs[j] / c;
-    double v = log(1.0 - p) - log(p);
-    if (v != v) v = 0.0;                                 // nan_to_num: NaN -> 0
-    else if (isinf(v)) v = v > 0 ? DBL_MAX : -DBL_MAX;  // +-inf -> +-max
-    llr[i] = v;
+// Sequential ascending sum of cnt LDS values v[idx(i)], i = 0..cnt-1, with
+// the loads issued 16 ahead of the dependent additions (the reference's
+// order; a one-lane chain otherwise waits on every LDS read).
+template <typename F>
+__device__ __forceinline__ double lds_seq_sum(const double* v, int cnt, F idx) {
+  double s = 0.0;
+  int i = 0;
+  for (; i + 16 <= cnt; i += 16) {
+    double r[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) r[u] = v[idx(i + u)];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += r[u];
   }
+  for (; i < cnt; ++i) s += v[idx(i)];
+  return s;
 }
 
-// bp2sp of the LDPC a-posteriori LLRs (sparc_ldpc.py:683-696 -> :283-314):
-// bp_t = 1/(1+exp(app_t)); sp_m = prod_t (bit_t(m) ? bp_t : 1 - bp_t), MSB
-// first.  Thread per (codeword, LDPC section, entry); unnormalised into sp.
-__global__ void k_bp2sp(const double* __restrict__ app, int M, int lgM, int ns, int B, double* __restrict__ sp) {
-  const size_t tot = (size_t)B * ns * M;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
-    const int m = (int)(i % M);
-    const size_t bl = i / M;  // b * ns + lp
-    const double* a = app + bl * lgM;
+// sp2bp + LLR (sparc_ldpc.py:470-479 -> :257-281): one wavefront per
+// (codeword, LDPC section).  The section's posterior beta_j / c_l is read once
+// (coalesced) into LDS; lane t < log2 M then forms p_t, the sum over the
+// entries j whose bit (logM-1-t) is set, in ascending j (the reference's
+// order); llr = nan_to_num(log(1 - p) - log(p)).
+template <typename real>
+__global__ void __launch_bounds__(64) k_llr(const real* __restrict__ beta, const double* __restrict__ cd, int L,
+                                            int M, int lgM, int l0, int ns, double* __restrict__ llr) {
+  extern __shared__ double post[];
+  const size_t bl = blockIdx.x;  // b * ns + lp
+  const int l = l0 + (int)(bl % ns);
+  const real* bs = beta + ((bl / ns) * L + l) * M;
+  const double c = cd[l];
+  for (int j = threadIdx.x; j < M; j += 64) post[j] = (double)bs[j] / c;
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= lgM) return;
+  const int sh = lgM - 1 - t, lo = (1 << sh) - 1;
+  // i-th entry (ascending) whose bit sh is set
+  const double p = lds_seq_sum(post, M >> 1, [=](int i) { return ((i >> sh) << (sh + 1)) | (lo + 1) | (i & lo); });
+  double v = log(1.0 - p) - log(p);
+  if (v != v) v = 0.0;                                 // nan_to_num: NaN -> 0
+  else if (isinf(v)) v = v > 0 ? DBL_MAX : -DBL_MAX;  // +-inf -> +-max
+  llr[bl * lgM + t] = v;
+}
+
+// bp2sp of the LDPC a-posteriori LLRs into beta0 (sparc_ldpc.py:683-696 ->
+// :283-314), one wavefront per (codeword, LDPC section): bp_t = 1/(1+exp(app_t));
+// sp_m = prod_t (bit_t(m) ? bp_t : 1 - bp_t), MSB first, in LDS; the
+// reference's sequential normaliser S (builtin sum, :313); beta0_m = (sp_m / S) c_l.
+template <typename real>
+__global__ void __launch_bounds__(64) k_soft_sec(const double* __restrict__ app, const double* __restrict__ cd,
+                                                 int L, int M, int lgM, int l0, int ns, real* __restrict__ beta) {
+  extern __shared__ double sp[];
+  __shared__ double bpv[32];
+  __shared__ double S;
+  const size_t bl = blockIdx.x;  // b * ns + lp
+  const int l = l0 + (int)(bl % ns);
+  if (threadIdx.x < lgM) bpv[threadIdx.x] = 1.0 / (1.0 + exp(app[bl * lgM + threadIdx.x]));
+  __syncthreads();
+  for (int m = threadIdx.x; m < M; m += 64) {
     double prod = 1.0;
     for (int t = 0; t < lgM; ++t) {
-      const double bp = 1.0 / (1.0 + exp(a[t]));
+      const double bp = bpv[t];
       prod *= ((m >> (lgM - 1 - t)) & 1) ? bp : 1.0 - bp;
     }
-    sp[i] = prod;
+    sp[m] = prod;
   }
-}
-
-// Normalise each LDPC section (builtin sum, sequential, :313) and scale by
-// c_l (:696) into beta0; thread per (codeword, LDPC section).
-template <typename real>
-__global__ void k_sp_norm(const double* __restrict__ sp, const double* __restrict__ cd, int L, int M, int l0,
-                          int ns, int B, real* __restrict__ beta) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * ns) return;
-  const int b = i / ns, lp = i % ns, l = l0 + lp;
-  const double* s = sp + (size_t)i * M;
-  double S = 0.0;
-  for (int m = 0; m < M; ++m) S += s[m];
-  real* o = beta + ((size_t)b * L + l) * M;
-  const double c = cd[l];
-  for (int m = 0; m < M; ++m) o[m] = (real)((s[m] / S) * c);
+  __syncthreads();
+  if (threadIdx.x == 0) S = lds_seq_sum(sp, M, [](int i) { return i; });
+  __syncthreads();
+  const double c = cd[l], tot = S;
+  real* o = beta + ((bl / ns) * L + l) * M;
+  for (int m = threadIdx.x; m < M; m += 64) o[m] = (real)((sp[m] / tot) * c);
 }
 
 // beta0 of the sections AMP keeps (:657, :691, :696): (beta / c) * c.
@@ -2529,24 +2761,21 @@ __global__ void __launch_bounds__(256) k_threshold(const double* __restrict__ ap
                                                    double thr, int32_t* __restrict__ idx) {
   extern __shared__ double sp[];
   __shared__ int cnt, pick;
-  __shared__ double S;
+  __shared__ double S, bpv[32];
   const size_t bl = blockIdx.x;  // b * ns + section
-  const double* a = app + bl * lgM;
+  if (threadIdx.x < lgM) bpv[threadIdx.x] = 1.0 / (1.0 + exp(app[bl * lgM + threadIdx.x]));
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
   for (int m = threadIdx.x; m < M; m += 256) {
     double prod = 1.0;
     for (int t = 0; t < lgM; ++t) {
-      const double bp = 1.0 / (1.0 + exp(a[t]));
+      const double bp = bpv[t];
       prod *= ((m >> (lgM - 1 - t)) & 1) ? bp : 1.0 - bp;
     }
     sp[m] = prod;
   }
-  if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0.0;
-    for (int m = 0; m < M; ++m) s += sp[m];
-    S = s;
-  }
+  if (threadIdx.x == 0) S = lds_seq_sum(sp, M, [](int i) { return i; });
   __syncthreads();
   for (int m = threadIdx.x; m < M; m += 256)
     if (sp[m] / S > thr) {
@@ -2562,12 +2791,15 @@ int grid_of(size_t tot) {
   return (int)(g < 65536 ? (g > 0 ? g : 1) : 65536);
 }
 
+constexpr int kGlueMaxM = 8192;  // a section of fp64 in the 64 KiB of dynamic LDS
+
 int check_glue(sa_ctx* c, int B, int l0, int ns) {
   if (check_ctx(c)) return SA_ERR_ARG;
   if (B <= 0 || B > c->Bcap) return fail(SA_ERR_ARG, "batch larger than the context's workspace");
   if (l0 < 0 || ns <= 0 || l0 + ns > c->L) return fail(SA_ERR_ARG, "section range outside [0, L)");
   if (!c->power_set) return fail(SA_ERR_ARG, "power allocation not staged");
   if (c->M < 2) return fail(SA_ERR_UNSUPPORTED, "M < 2 carries no bits");
+  if (c->M > kGlueMaxM) return fail(SA_ERR_UNSUPPORTED, "SPARC<->LDPC glue stages a section in LDS: M <= 8192");
   return SA_OK;
 }
 
@@ -2626,6 +2858,7 @@ void sa_destroy(sa_ctx* c) {
   free_workspace(c);
   dev_free(c->d_inv);
   dev_free(c->d_fwd);
+  dev_free(c->d_fwd2);
   dev_free(c->d_A);
   dev_free(c->d_c);
   dev_free(c->d_cd);
@@ -2865,10 +3098,11 @@ int sa_llr(sa_ctx* c, int B, int l0, int ns, double* llr, int flags) {
     if ((rc = ensure_stage(c, cnt))) return rc;
     d_out = c->d_stage;
   }
+  const size_t lds = (size_t)c->M * sizeof(double);
   if (c->prec == SA_PREC_F64)
-    k_llr<double><<<grid_of(cnt), 256, 0, c->stream>>>((const double*)c->d_beta, c->d_cd, c->L, c->M, lgM, l0, ns, B, d_out);
+    k_llr<double><<<B * ns, 64, lds, c->stream>>>((const double*)c->d_beta, c->d_cd, c->L, c->M, lgM, l0, ns, d_out);
   else
-    k_llr<float><<<grid_of(cnt), 256, 0, c->stream>>>((const float*)c->d_beta, c->d_cd, c->L, c->M, lgM, l0, ns, B, d_out);
+    k_llr<float><<<B * ns, 64, lds, c->stream>>>((const float*)c->d_beta, c->d_cd, c->L, c->M, lgM, l0, ns, d_out);
   HIP_TRY(hipGetLastError());
   if (!(flags & SA_PTR_DEVICE)) HIP_TRY(hipMemcpyAsync(llr, d_out, cnt * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2881,25 +3115,20 @@ int sa_soft_beta0(sa_ctx* c, int B, int l0, int ns, const double* app, int flags
   if (!app) return fail(SA_ERR_ARG, "sa_soft_beta0: app is NULL");
   HIP_TRY(hipSetDevice(c->device));
   const int lgM = ilog2(c->M);
-  const size_t na = (size_t)B * ns * lgM, nsp = (size_t)B * ns * c->M;
-  // staging layout: [app copy (host input only)] [sp]
-  const size_t off = (flags & SA_PTR_DEVICE) ? 0 : na;
-  if ((rc = ensure_stage(c, off + nsp))) return rc;
+  const size_t na = (size_t)B * ns * lgM;
   const double* d_app = app;
   if (!(flags & SA_PTR_DEVICE)) {
+    if ((rc = ensure_stage(c, na))) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_stage, app, na * 8, hipMemcpyHostToDevice, c->stream));
     d_app = c->d_stage;
   }
-  double* sp = c->d_stage + off;
-  k_bp2sp<<<grid_of(nsp), 256, 0, c->stream>>>(d_app, c->M, lgM, ns, B, sp);
-  const int nb = (B * ns + 255) / 256;
-  const size_t tot = (size_t)B * c->L * c->M;
+  const size_t tot = (size_t)B * c->L * c->M, lds = (size_t)c->M * sizeof(double);
   if (c->prec == SA_PREC_F64) {
-    k_rescale<double><<<grid_of(tot), 256, 0, c->stream>>>((double*)c->d_beta, c->d_cd, c->L, c->M, l0, ns, B);
-    k_sp_norm<double><<<nb, 256, 0, c->stream>>>(sp, c->d_cd, c->L, c->M, l0, ns, B, (double*)c->d_beta);
+    if (ns < c->L) k_rescale<double><<<grid_of(tot), 256, 0, c->stream>>>((double*)c->d_beta, c->d_cd, c->L, c->M, l0, ns, B);
+    k_soft_sec<double><<<B * ns, 64, lds, c->stream>>>(d_app, c->d_cd, c->L, c->M, lgM, l0, ns, (double*)c->d_beta);
   } else {
-    k_rescale<float><<<grid_of(tot), 256, 0, c->stream>>>((float*)c->d_beta, c->d_cd, c->L, c->M, l0, ns, B);
-    k_sp_norm<float><<<nb, 256, 0, c->stream>>>(sp, c->d_cd, c->L, c->M, l0, ns, B, (float*)c->d_beta);
+    if (ns < c->L) k_rescale<float><<<grid_of(tot), 256, 0, c->stream>>>((float*)c->d_beta, c->d_cd, c->L, c->M, l0, ns, B);
+    k_soft_sec<float><<<B * ns, 64, lds, c->stream>>>(d_app, c->d_cd, c->L, c->M, lgM, l0, ns, (float*)c->d_beta);
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2972,7 +3201,7 @@ int sa_plan(sa_ctx* c, int B, int64_t* o) {
   const bool dense = c->backend == SA_BACKEND_DENSE;
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
-  o[0] = dense ? 3 : (batched ? 2 : (sec2 ? 1 : 0));
+  o[0] = dense ? 3 : (batched ? 2 : (sec2 ? (c->sec4 ? 4 : 1) : 0));
   o[1] = dense ? c->KS : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
   o[3] = batched ? c->CB : 1;

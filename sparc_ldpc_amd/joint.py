@@ -130,12 +130,28 @@ class JointDecoder:
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         idx = np.ascontiguousarray(idx, dtype=np.int32)
+        self.stage(idx, noise, Pl)
+        return self.decode_staged(idx, Pl, mode, soft_iter)
+
+    def stage(self, idx, noise, Pl):
+        """Encode on the device: y = A beta(idx) + noise becomes the staged input."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        B = idx.shape[0]
+        self.op.reserve(B, self.T)
+        if self.sub is not None:
+            self.sub.reserve(B, self.T)
+        self.op.stage_power(B, np.asarray(Pl, dtype=np.float64))
+        self.op.encode(idx, noise)
+        self.code.device_buffers(B)
+
+    def decode_staged(self, idx, Pl, mode="soft", soft_iter=2):
+        """The joint decode of the staged batch (see run); idx only scores the decisions."""
+        if mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}")
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
         B = idx.shape[0]
         Pl = np.asarray(Pl, dtype=np.float64)
         op, T, l0 = self.op, self.T, self.l0
-        op.reserve(B, T)
-        op.stage_power(B, Pl)
-        op.encode(idx, noise)
         op.run(B, T)
         op.wait()
         rx = op.decide(B)
@@ -146,8 +162,6 @@ class JointDecoder:
         if mode == "originalHard":
             d_app = self._bp(B)
             bp_iters.append(self.code.fetch_buffers(B, app=False)[1])
-            if l0 > 0:
-                self.sub.reserve(B, T)
             idx_l = op.hard_cancel(B, l0, self.ns, d_app, dst=self.sub if l0 > 0 else None)
             dec = rx.copy()
             dec[:, l0:] = idx_l

@@ -213,7 +213,7 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, dptr(out), iters.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return out, iters
 
-    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense")
+    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4")
 
     def plan(self, B):
         """Which kernels a decode of B codewords runs (sa_plan)."""

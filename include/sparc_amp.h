@@ -105,6 +105,12 @@ double sa_run_event_ms(sa_ctx* ctx);
  * 2 dense A^T z GEMV, 3 dense denoiser, 4 dense A beta GEMV; out[10] = total
  * ms of the sequence.  Leaves the decode's results in place like sa_run. */
 int sa_profile(sa_ctx* ctx, int B, int T, int flags, double* out);
+/* The same with every bracketed launch issued `rep` (1..1024) times back to
+ * back between its events: mean = elapsed / rep, i.e. the launch's duration
+ * plus the same-stream kernel boundary, without the event packets' dispatch
+ * overhead.  The results left in place are then those of repeated
+ * launches (not a decode); re-run sa_run before fetching. */
+int sa_profile_rep(sa_ctx* ctx, int B, int T, int flags, int rep, double* out);
 
 /* Per-codeword section decisions (sparc_ldpc.py:452-455: argmax per
  * section, first index on ties) of the last sa_run / sa_amp, computed on

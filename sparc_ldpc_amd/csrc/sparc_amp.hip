@@ -1813,8 +1813,12 @@ int ilog2(int x) {
 }  // namespace
 
 // Per-launch HIP-event bracketing for sa_profile (eager sequence only).
+// With rep > 1 every bracketed launch is issued rep times back to back
+// between its two events (sa_profile_rep: mean = elapsed / rep), which
+// excludes the event packets' own dispatch overhead from the per-launch time.
 struct Prof {
   std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> ev;
+  int rep = 1;
   int begin(hipStream_t s, int kind) {
     hipEvent_t a = nullptr, b = nullptr;
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
@@ -1831,6 +1835,8 @@ struct Prof {
 };
 
 enum { K_SEC = 0, K_ROW = 1, K_DAZ = 2, K_DDEN = 3, K_DAB = 4, K_NKINDS = 5 };
+
+#define PROF_REPS(c) for (int _rep = 0, _nrep = (c)->prof ? (c)->prof->rep : 1; _rep < _nrep; ++_rep)
 
 struct sa_ctx {
   Prof* prof = nullptr;
@@ -2035,7 +2041,7 @@ void launch_sec_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.RS = row_splits(c, B);
   dim3 grid(c->G * a.RS, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
-  k_sec<real, E><<<grid, 256, c->sec_lds, c->stream>>>(a);
+  PROF_REPS(c) k_sec<real, E><<<grid, 256, c->sec_lds, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
 }
 
@@ -2046,7 +2052,7 @@ void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.B = B;
   a.NC = (B + CB - 1) / CB;
   if (c->prof) c->prof->begin(c->stream, K_SEC);
-  k_secb<real, E, CB, kWB><<<c->Gb * a.NC, kWB * 64, c->secb_lds, c->stream>>>(a);
+  PROF_REPS(c) k_secb<real, E, CB, kWB><<<c->Gb * a.NC, kWB * 64, c->secb_lds, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
 }
 
@@ -2101,11 +2107,11 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout) {
   if (c->prof) c->prof->begin(c->stream, K_SEC);
   if (c->sec4) {
     switch (c->M / 256) {
-      case 1: k_sec4<real, 1><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 2: k_sec4<real, 2><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 4: k_sec4<real, 4><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 8: k_sec4<real, 8><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 16: k_sec4<real, 16><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 1: PROF_REPS(c) k_sec4<real, 1><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 2: PROF_REPS(c) k_sec4<real, 2><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 4: PROF_REPS(c) k_sec4<real, 4><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 8: PROF_REPS(c) k_sec4<real, 8><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 16: PROF_REPS(c) k_sec4<real, 16><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
       default: return fail(SA_ERR_UNSUPPORTED, "k_sec4: M");
     }
     if (c->prof) c->prof->end(c->stream);
@@ -2113,12 +2119,12 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout) {
     return SA_OK;
   }
   switch (c->M / 128) {
-    case 1: k_sec2<real, 1><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 2: k_sec2<real, 2><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 4: k_sec2<real, 4><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 8: k_sec2<real, 8><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 16: k_sec2<real, 16><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 32: k_sec2<real, 32><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 1: PROF_REPS(c) k_sec2<real, 1><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 2: PROF_REPS(c) k_sec2<real, 2><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 4: PROF_REPS(c) k_sec2<real, 4><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 8: PROF_REPS(c) k_sec2<real, 8><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 16: PROF_REPS(c) k_sec2<real, 16><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 32: PROF_REPS(c) k_sec2<real, 32><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
     default: return fail(SA_ERR_UNSUPPORTED, "k_sec2: M");
   }
   if (c->prof) c->prof->end(c->stream);
@@ -2152,9 +2158,9 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb) {
   // small batch: 16-row workgroups cover the chip; many codewords: 64-row
   // workgroups, 4 waves with deeper per-lane load streams
   if (c->nz_cur == c->NZ16)
-    k_row2<real><<<dim3(c->NZ16, B), 16 * kRow2Rows, 0, c->stream>>>(a);
+    PROF_REPS(c) k_row2<real><<<dim3(c->NZ16, B), 16 * kRow2Rows, 0, c->stream>>>(a);
   else
-    k_row<real, 4><<<dim3(c->NZ, B), 4 * 64, 0, c->stream>>>(a);
+    PROF_REPS(c) k_row<real, 4><<<dim3(c->NZ, B), 4 * 64, 0, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -2174,7 +2180,7 @@ int launch_dense_az(sa_ctx* c, int B, int t, int es, int mode) {
   DenseArgs a = dense_args(c, t, es, mode);
   dim3 grid((unsigned)((c->lda / 4 + 255) / 256), c->RS, B);
   if (c->prof) c->prof->begin(c->stream, K_DAZ);
-  k_dense_az<<<grid, 256, 0, c->stream>>>(a);
+  PROF_REPS(c) k_dense_az<<<grid, 256, 0, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -2184,7 +2190,7 @@ int launch_dense_ab(sa_ctx* c, int B, int t, int es, int mode) {
   DenseArgs a = dense_args(c, t, es, mode);
   dim3 grid((unsigned)((c->n + kDenseRows - 1) / kDenseRows), c->KS, B);
   if (c->prof) c->prof->begin(c->stream, K_DAB);
-  k_dense_ab<<<grid, 256, 0, c->stream>>>(a, (const float*)c->d_tau);
+  PROF_REPS(c) k_dense_ab<<<grid, 256, 0, c->stream>>>(a, (const float*)c->d_tau);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -2194,7 +2200,7 @@ template <int E>
 void launch_dense_den_e(sa_ctx* c, int B, const DenseArgs& a) {
   dim3 grid(c->Gd, B);
   if (c->prof) c->prof->begin(c->stream, K_DDEN);
-  k_dense_den<E><<<grid, 256, 0, c->stream>>>(a, (const float*)c->d_c, (float*)c->d_beta,
+  PROF_REPS(c) k_dense_den<E><<<grid, 256, 0, c->stream>>>(a, (const float*)c->d_c, (float*)c->d_beta,
                                                (float*)c->d_bbp, (float*)c->d_tau, c->d_iters, c->Gd);
   if (c->prof) c->prof->end(c->stream);
 }
@@ -2984,14 +2990,17 @@ int sa_amp(sa_ctx* c, int B, const double* y, const double* Pl, int T, const dou
   return sa_fetch(c, B, beta_out, iters_out);
 }
 
-int sa_profile(sa_ctx* c, int B, int T, int flags, double* out) {
+int sa_profile(sa_ctx* c, int B, int T, int flags, double* out) { return sa_profile_rep(c, B, T, flags, 1, out); }
+
+int sa_profile_rep(sa_ctx* c, int B, int T, int flags, int rep, double* out) {
   if (check_ctx(c)) return SA_ERR_ARG;
-  if (B <= 0 || T <= 0 || !out || B > c->Bcap || T > c->Tcap || !c->power_set)
+  if (B <= 0 || T <= 0 || !out || B > c->Bcap || T > c->Tcap || !c->power_set || rep < 1 || rep > 1024)
     return fail(SA_ERR_ARG, "sa_profile: bad arguments (reserve and stage first)");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (int rcb = ensure_beta2(c, B)) return rcb;
   Prof prof;
+  prof.rep = rep;
   c->prof = &prof;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIP_TRY(hipEventCreate(&e0));
@@ -3009,7 +3018,7 @@ int sa_profile(sa_ctx* c, int B, int T, int flags, double* out) {
     for (auto& ev : prof.ev) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, std::get<1>(ev), std::get<2>(ev)) == hipSuccess) {
-        sum[std::get<0>(ev)] += ms;
+        sum[std::get<0>(ev)] += ms / rep;
         cnt[std::get<0>(ev)] += 1;
       }
     }

@@ -199,11 +199,13 @@ class SparcOperator:
 
     KERNEL_KINDS = ("k_sec", "k_row", "k_dense_az", "k_dense_den", "k_dense_ab")
 
-    def profile(self, B, T, early_stop=True, beta0=False):
-        """Eager decode with per-launch HIP events: {kind: (mean_ms, launches)}, total_ms."""
+    def profile(self, B, T, early_stop=True, beta0=False, rep=1):
+        """Eager decode with per-launch HIP events: {kind: (mean_ms, launches)}, total_ms.
+        rep > 1: each launch issued rep times back to back between its events
+        (mean = elapsed / rep; the staged results are then not a decode)."""
         flags = (0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP) | (_lib.SA_FLAG_BETA0 if beta0 else 0)
         out = np.zeros(11)
-        check(self._lib.sa_profile(self._ctx, int(B), int(T), flags, dptr(out)))
+        check(self._lib.sa_profile_rep(self._ctx, int(B), int(T), flags, int(rep), dptr(out)))
         kinds = {k: (float(out[2 * i]), int(out[2 * i + 1])) for i, k in enumerate(self.KERNEL_KINDS)}
         return kinds, float(out[10])
 

@@ -66,6 +66,14 @@ __device__ __forceinline__ float4 ld_stream(const float* p) {
 }
 
 
+// Store of a partial another kernel reads after the boundary (Ab partials):
+// non-temporal, so no dirty L2 line is left for the kernel-end writeback to
+// drain (c2: k_sec4 7.85 -> 7.65 us, +1.5 % codewords/s; c3 neutral).
+template <typename T>
+__device__ __forceinline__ void st_part(T* p, T v) {
+  __builtin_nontemporal_store(v, p);
+}
+
 // ---------------------------------------------------------------------------
 // Device helpers
 // ---------------------------------------------------------------------------
@@ -638,7 +646,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
 #pragma unroll
     for (int u = 0; u < KR; ++u) {
       const int r = r0 + u * 256 + tid;
-      if (r < rb1) abp[r] = acc[u];
+      if (r < rb1) st_part(&abp[r], acc[u]);
     }
     if (more) {
 #pragma unroll
@@ -834,7 +842,7 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
         const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
         real t = (e & 0x8000u) ? -v0 : v0;
         t += (e & 0x80000000u) ? -v1 : v1;
-        abp[r] = t;
+        st_part(&abp[r], t);
       }
     }
   }
@@ -844,41 +852,63 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
   STAMP(9);
 #endif
 }
-// Four wavefronts per section (k_sec4): the k_sec2 workgroup of two sections
-// with 512 threads.  Wave q of a section holds quarter q (the two top index
-// bits); the two top FWHT stages cross the quarters in one LDS exchange with
-// the additions of two single-bit stages, ((x0 +- x1) +- (x2 +- x3)), so the
-// transform is bit-identical to k_sec2's.  Per wave the LDS gather chain and
-// the Ab row loop are half as long, and every SIMD runs two waves.
-template <typename real, int E4>
-__device__ __forceinline__ void top2_stage(real (&v)[E4], real* xs, int lane, int q) {
-  constexpr int QS = E4 * 64;  // one quarter
+// QW wavefronts per section (k_sec4: QW = 4): the k_sec2
+// workgroup of two sections with 2*QW waves.  Wave q of a section holds the
+// q-th 1/QW of it (the log2(QW) top index bits); those top FWHT stages cross
+// the waves in one LDS exchange, applied lowest bit first like the
+// single-bit stages ((x0 +- x1) +- (x2 +- x3)) ..., so the transform is
+// bit-identical to k_sec2's.  Per wave the LDS gather chain and the Ab row
+// loop shrink with QW, and every SIMD runs QW / 2 waves.  (QW = 8, 1024-thread
+// workgroups, measured slower at c2: 8.1 vs 7.6 us per launch.)
+template <typename real, int EQ, int QW>
+__device__ __forceinline__ void topq_stage(real (&v)[EQ], real* xs, int lane, int q) {
+  constexpr int QS = EQ * 64;  // one wave's share of the section
 #pragma unroll
-  for (int i = 0; i < E4; ++i) xs[q * QS + i * 64 + lane] = v[i];
+  for (int i = 0; i < EQ; ++i) xs[q * QS + i * 64 + lane] = v[i];
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < E4; ++i) {
-    const real x0 = xs[i * 64 + lane], x1 = xs[QS + i * 64 + lane];
-    const real x2 = xs[2 * QS + i * 64 + lane], x3 = xs[3 * QS + i * 64 + lane];
-    const real lo = (q & 1) ? x0 - x1 : x0 + x1;
-    const real hi = (q & 1) ? x2 - x3 : x2 + x3;
-    v[i] = (q & 2) ? lo - hi : lo + hi;
+  for (int i = 0; i < EQ; ++i) {
+    real x[QW];
+#pragma unroll
+    for (int j = 0; j < QW; ++j) x[j] = xs[j * QS + i * 64 + lane];
+#pragma unroll
+    for (int k = 0, span = 1; span < QW; ++k, span <<= 1)
+#pragma unroll
+      for (int j = 0; j < QW; j += 2 * span) x[j] = ((q >> k) & 1) ? x[j] - x[j + span] : x[j] + x[j + span];
+    v[i] = x[0];
   }
   __syncthreads();
 }
 
-template <typename real, int E4>
-__global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
+// Fixed-order combination of the QW per-wave values red[(w0 + j) * 4 + f]
+// of one section: max, or a pairwise tree sum ((r0 + r1) + (r2 + r3)) ...
+template <typename real, int QW, bool MAX>
+__device__ __forceinline__ real combine_q(const real* red, int w0, int f) {
+  real x[QW];
+#pragma unroll
+  for (int j = 0; j < QW; ++j) x[j] = red[(w0 + j) * 4 + f];
+#pragma unroll
+  for (int span = 1; span < QW; span <<= 1)
+#pragma unroll
+    for (int j = 0; j < QW; j += 2 * span) {
+      if constexpr (MAX) x[j] = x[j] > x[j + span] ? x[j] : x[j + span];
+      else x[j] = x[j] + x[j + span];
+    }
+  return x[0];
+}
+
+template <typename real, int EQ, int QW>
+__device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NT = 512;
-  constexpr int KH = E4 >= 8 ? 4 : 16;
-  constexpr int NQ = (E4 + 3) / 4;
-  constexpr int KR = 9;  // rows per thread per pass: n <= 4608 in one pass
+  constexpr int NT = 2 * QW * 64;
+  constexpr int KH = EQ >= 8 ? 4 : 16;
+  constexpr int NQ = (EQ + 3) / 4;
+  constexpr int KR = (4608 + NT - 1) / NT;  // rows per thread per pass: n <= 4608 in one pass
   const int g = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int sidx = wv >> 2, q = wv & 3;
-  const int M = a.M, n = a.n, Mq = M >> 2;
+  const int sidx = wv / QW, q = wv % QW;
+  const int M = a.M, n = a.n, Mq = M / QW;
   const size_t LM = (size_t)a.L * M;
   const int l = g * 2 + sidx;
   const bool have = l < a.L;
@@ -889,10 +919,10 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
   const int zslots = ((n + 1) * (int)sizeof(real) + 15) / 16 * 16 / (int)sizeof(real);
   real* ts = zs + zslots;          // [2][M]   T_l = H_M beta_l
   real* xb = ts + 2 * M;           // [2][M]   top-stage exchange, one M per section
-  real* red = xb + 2 * M;          // [8][4]   per-wave max, S, S2, beta^2
+  real* red = xb + 2 * M;          // [2*QW][4] per-wave max, S, S2, beta^2
 
-  real v[E4];
-  real bprev[E4];
+  real v[EQ];
+  real bprev[EQ];
   const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
   real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
   const uint16_t* il = a.inv + (size_t)lc * a.w + eoff;
@@ -908,8 +938,8 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
   const real* zb = a.z + (size_t)b * n;
   ZStage<real, NT> zst;
   zst.issue(zb, n, tid);
-  load_buckets<E4, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
-  load_section<real, E4>(bl, bprev, lane, Mq);
+  load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
+  load_section<real, EQ>(bl, bprev, lane, Mq);
   const real cl = a.c[lc];
   const int nk = min(KR, (n + NT - 1) / NT);
 #pragma unroll
@@ -931,12 +961,12 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
   STAMP(2);
 
 #pragma unroll
-  for (int i = 0; i < E4; ++i) v[i] = 0;
+  for (int i = 0; i < EQ; ++i) v[i] = 0;
   for (int h0 = 0; h0 < a.nhi; h0 += KH) {
     ushort4 tn[KH][NQ];
     const bool more = h0 + KH < a.nhi;
-    if (more) load_buckets<E4, KH>(il, h0 + KH, a.nhi, M, lane, tn);
-    gather_buckets<real, E4, KH>(zs, h0, a.nhi, tb, v);
+    if (more) load_buckets<EQ, KH>(il, h0 + KH, a.nhi, M, lane, tn);
+    gather_buckets<real, EQ, KH>(zs, h0, a.nhi, tb, v);
     if (more) {
 #pragma unroll
       for (int hh = 0; hh < KH; ++hh)
@@ -946,8 +976,8 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
   }
   real* xs = xb + sidx * M;
   STAMP(3);
-  fwht_wave<real, E4>(v, lane, 64);
-  top2_stage<real, E4>(v, xs, lane, q);
+  fwht_wave<real, EQ>(v, lane, 64);
+  topq_stage<real, EQ, QW>(v, xs, lane, q);
   STAMP(4);
 
   // denoiser (sparc_ldpc.py:213-219) over the four quarters of the section
@@ -955,22 +985,18 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
   const real kk = cl / tau2;
   real mx = neg_inf<real>();
 #pragma unroll
-  for (int i = 0; i < E4; ++i) {
+  for (int i = 0; i < EQ; ++i) {
     v[i] = fma(v[i], inv_sn, bprev[i]) * kk;
     mx = v[i] > mx ? v[i] : mx;
   }
   mx = wave_max(mx);
   if (lane == 0) red[wv * 4] = mx;
   __syncthreads();
-  const int w0 = wv & ~3;
-  {
-    const real m01 = red[w0 * 4] > red[(w0 + 1) * 4] ? red[w0 * 4] : red[(w0 + 1) * 4];
-    const real m23 = red[(w0 + 2) * 4] > red[(w0 + 3) * 4] ? red[(w0 + 2) * 4] : red[(w0 + 3) * 4];
-    mx = m01 > m23 ? m01 : m23;
-  }
+  const int w0 = wv & ~(QW - 1);
+  mx = combine_q<real, QW, true>(red, w0, 0);
   real S = 0, S2 = 0;
 #pragma unroll
-  for (int i = 0; i < E4; ++i) {
+  for (int i = 0; i < EQ; ++i) {
     v[i] = dexp<real>(v[i] - mx);
     S += v[i];
     S2 += v[i] * v[i];
@@ -981,27 +1007,27 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
     red[wv * 4 + 2] = S2;
   }
   __syncthreads();
-  S = (red[w0 * 4 + 1] + red[(w0 + 1) * 4 + 1]) + (red[(w0 + 2) * 4 + 1] + red[(w0 + 3) * 4 + 1]);
-  S2 = (red[w0 * 4 + 2] + red[(w0 + 1) * 4 + 2]) + (red[(w0 + 2) * 4 + 2] + red[(w0 + 3) * 4 + 2]);
+  S = combine_q<real, QW, false>(red, w0, 1);
+  S2 = combine_q<real, QW, false>(red, w0, 2);
   const real scale = cl / S;
 #pragma unroll
-  for (int i = 0; i < E4; ++i) v[i] = have ? v[i] * scale : (real)0;
-  if (have) store_section<real, E4>(blo, v, lane, Mq);
+  for (int i = 0; i < EQ; ++i) v[i] = have ? v[i] * scale : (real)0;
+  if (have) store_section<real, EQ>(blo, v, lane, Mq);
   const real bb = have ? S2 * scale * scale : (real)0;
 
   STAMP(5);
-  fwht_wave<real, E4>(v, lane, 64);  // T_l = H_M beta_l
-  top2_stage<real, E4>(v, xs, lane, q);
+  fwht_wave<real, EQ>(v, lane, 64);  // T_l = H_M beta_l
+  topq_stage<real, EQ, QW>(v, xs, lane, q);
   STAMP(6);
   {
     real* tl = ts + sidx * M + eoff;
 #pragma unroll
-    for (int i = 0; i < E4; ++i) tl[elem_index<E4>(lane, i)] = v[i];
+    for (int i = 0; i < EQ; ++i) tl[elem_index<EQ>(lane, i)] = v[i];
   }
   if (lane == 0) red[wv * 4 + 3] = bb;
   __syncthreads();
   STAMP(7);
-  if (tid == 0) a.bbp[(size_t)b * a.G + g] = red[0 * 4 + 3] + red[4 * 4 + 3];
+  if (tid == 0) a.bbp[(size_t)b * a.G + g] = red[0 * 4 + 3] + red[QW * 4 + 3];
   // Ab partial of the pair for every row
   real* abp = a.abp + ((size_t)b * a.G + g) * n;
   for (int r0 = 0; r0 < n; r0 += NT * KR) {
@@ -1021,7 +1047,7 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
         const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
         real t = (e & 0x8000u) ? -v0 : v0;
         t += (e & 0x80000000u) ? -v1 : v1;
-        abp[r] = t;
+        st_part(&abp[r], t);
       }
     }
   }
@@ -1031,6 +1057,9 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) {
   STAMP(9);
 #endif
 }
+
+template <typename real, int E4>
+__global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) { secq_body<real, E4, 4>(a); }
 // ---------------------------------------------------------------------------
 // Batched section kernel (B codewords share the operator)
 // ---------------------------------------------------------------------------
@@ -1374,7 +1403,7 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
       if (r < n) {
 #pragma unroll
         for (int c = 0; c < CB; ++c)
-          if (live[c]) a.abp[((size_t)bc[c] * a.G + g) * n + r] = acc[c];
+          if (live[c]) st_part(&a.abp[((size_t)bc[c] * a.G + g) * n + r], acc[c]);
       }
     }
     if (more) {

@@ -1,5 +1,7 @@
-"""Diagnostic: phase shares of k_sec from s_memtime stamps (workgroup 0).
-Run with SPARC_AMP_LIB=sparc_ldpc_amd/libsparc_amp_stamps.so on the GPU box."""
+"""Diagnostic: phase shares of the single-codeword section kernel (k_sec4)
+from s_memtime stamps of workgroup 0, wave 0 (cycles at the shader clock).
+Run with SPARC_AMP_LIB=sparc_ldpc_amd/libsparc_amp_stamps.so on the GPU box
+(`make -C sparc_ldpc_amd/csrc stamps`)."""
 import ctypes as ct
 import sys
 import os
@@ -17,15 +19,19 @@ y = synth_y(op, Pl, w["sigma"], list(range(B)))
 op.reserve(B, T); op.stage(y, Pl)
 lib = sp.load_library()
 lib.sa_debug_stamps.argtypes = [ct.POINTER(ct.c_ulonglong)]
-names = ["issue", "tau+loads", "z->LDS+bar", "gather", "fwht1", "denoise", "fwht2", "ts+bar", "rows", "drain"]
-acc = np.zeros(9)
+# stamp order in time (index 10: after an explicit wait for every global load
+# issued so far, i.e. the bucket-table / previous-beta / Ab-table loads)
+order = [0, 1, 2, 10, 3, 4, 5, 6, 7, 8, 9]
+names = ["tau+loads", "z->LDS+bar", "wait tables", "gather", "fwht1", "denoise", "fwht2", "ts+bar", "rows",
+         "drain"]
+acc = np.zeros(len(order) - 1)
 for rep in range(20):
     op.run(B, T, early_stop=False); op.wait()
     st = (ct.c_ulonglong * 16)()
     lib.sa_debug_stamps(st)
-    v = np.array(st[:10], dtype=np.float64)
+    v = np.array([st[i] for i in order], dtype=np.float64)
     acc += np.diff(v)
 acc /= 20
-for nm, c in zip(names[1:], acc):
+for nm, c in zip(names, acc):
     print(f"{nm:12s} {c:9.0f} cycles  {c / acc.sum() * 100:5.1f}%")
 print(f"total {acc.sum():.0f} cycles")

@@ -959,6 +959,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   zst.store(zs, zb, n, tid);
   __syncthreads();
   STAMP(2);
+#ifdef SA_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: table loads landed
+  STAMP(10);
+#endif
 
 #pragma unroll
   for (int i = 0; i < EQ; ++i) v[i] = 0;

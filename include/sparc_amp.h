@@ -94,6 +94,14 @@ int sa_amp(sa_ctx* ctx, int B, const double* y, const double* Pl, int T,
  * last sa_run measured with HIP events on the context's stream. */
 int sa_reserve(sa_ctx* ctx, int B, int T);
 int sa_stage(sa_ctx* ctx, int B, const double* y, const double* Pl, const double* beta0);
+/* Per-codeword power allocations Pl [B][L] (Hadamard backend) for the next
+ * sa_run of up to B codewords: c_{b,l} = sqrt(n Pl_{b,l}), P_b = sum_l Pl_{b,l}
+ * (sparc_ldpc.py:190,214).  Sections with Pl = 0 keep beta = 0 and drop out
+ * of A beta, so this is the reference's shortened-operator decode
+ * (sparc_transforms_shorter, amp_exit.py:113-116) as a per-codeword section
+ * mask.  The binary64 glue kernels (sa_llr, ...) keep the c_l of the last
+ * sa_stage Pl; a later sa_stage with Pl returns to one allocation. */
+int sa_stage_power_batch(sa_ctx* ctx, int B, const double* Pl);
 int sa_run(sa_ctx* ctx, int B, int T, int flags);
 int sa_wait(sa_ctx* ctx);
 int sa_fetch(sa_ctx* ctx, int B, double* beta_out, int* iters_out);

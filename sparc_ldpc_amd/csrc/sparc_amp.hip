@@ -347,7 +347,7 @@ struct SecArgs {
   const uint16_t* __restrict__ inv;  // [L][w]  row of ordering value o, or n (zero slot)
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
-  const real* __restrict__ c;        // [L]     sqrt(n * Pl)
+  const real* __restrict__ c;        // [L] sqrt(n * Pl), or [B][L] per codeword (cst = L)
   const real* __restrict__ z;        // [B][n]
   real* __restrict__ beta;           // [B][L*M] previous estimate (read)
   real* __restrict__ beta_out;       // [B][L*M] new estimate (k_sec: the other ping-pong buffer)
@@ -358,6 +358,7 @@ struct SecArgs {
   real* __restrict__ tau;            // [B][T1]
   int* __restrict__ iters;           // [B]
   int L, M, n, w, nhi, G, NZ, T1, t, mode, early_stop;
+  int cst;  // codeword stride of c: 0 (one power allocation) or L (sa_stage_power_batch)
   int RS;  // row splits: RS workgroups share a section group, each gathers n/RS rows of Ab
   int B, NC;  // batched kernel: codewords, codeword chunks of CB
   real sqrt_n;
@@ -540,7 +541,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     zst.issue(zb, n, tid);
     load_buckets<E, KH>(il, 0, a.nhi, M, lane, tb);
     if (a.mode == SEC_AMP) load_section<real, E>(bl, bprev, lane, M);
-    const real cl = a.c[lc];
+    const real cl = a.c[(size_t)b * a.cst + lc];
     if (a.mode == SEC_AMP) {
 #pragma unroll
       for (int u = 0; u < KR; ++u) {
@@ -733,7 +734,7 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
   zst.issue(zb, n, tid);
   load_buckets<E2, KH>(il, 0, a.nhi, M, lane, tb);
   load_section<real, E2>(bl, bprev, lane, Mh);
-  const real cl = a.c[lc];
+  const real cl = a.c[(size_t)b * a.cst + lc];
   const int nk = min(KR, (n + 255) / 256);  // passes of 256 rows in the first chunk
 #pragma unroll
   for (int u = 0; u < KR; ++u) {
@@ -940,7 +941,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   zst.issue(zb, n, tid);
   load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
   load_section<real, EQ>(bl, bprev, lane, Mq);
-  const real cl = a.c[lc];
+  const real cl = a.c[(size_t)b * a.cst + lc];
   const int nk = min(KR, (n + NT - 1) / NT);
 #pragma unroll
   for (int u = 0; u < KR; ++u) {
@@ -1236,7 +1237,9 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
   } else {
     load_section<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lane, M);
   }
-  const real cl = a.c[lc];
+  real cl[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) cl[c] = a.c[(size_t)bc[c] * a.cst + lc];
   const ushort4* fw = a.fwd + (size_t)g * W4 * n;
   ushort4 f[KR][W4];
 #pragma unroll
@@ -1335,7 +1338,7 @@ __global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
     }
     fwht_wave<real, E>(v[c], lane, mlanes);
     real* bl = a.beta + (size_t)bc[c] * LM + (size_t)lc * M;
-    bbl[c] = denoise_section<real, E>(v[c], bprev[PB ? c : (c & 1)], bl, lane, M, cl, tau2[c], a.sqrt_n,
+    bbl[c] = denoise_section<real, E>(v[c], bprev[PB ? c : (c & 1)], bl, lane, M, cl[c], tau2[c], a.sqrt_n,
                                       have && live[c]);
     if (have) {
       fwht_wave<real, E>(v[c], lane, mlanes);  // T_l = H_M beta_l
@@ -1435,6 +1438,7 @@ struct RowArgs {
   real* __restrict__ out;        // [B][n] (ROW_ABOUT)
   int n, G, Gb, NZ, T1, t, mode, early_stop;  // G Ab partials, Gb beta^2 partials
   real sqrt_n, P;
+  const real* __restrict__ Pb;   // [B] per-codeword P (sa_stage_power_batch), or null: P
 };
 
 // Residual update with the Onsager term (sparc_ldpc.py:220):
@@ -1490,7 +1494,7 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   real ons = 0;
   if (a.mode == ROW_AMP) {
     const real bb = a.Gb <= 128 ? wave_sum_pair(bbv[0], bbv[1]) : wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
-    ons = a.P - bb / (real)n;
+    ons = (a.Pb ? a.Pb[b] : a.P) - bb / (real)n;
   }
   real zn = 0;
   if (r < n) {
@@ -1576,7 +1580,7 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
     } else {
       bb = wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
     }
-    ons = a.P - bb / (real)n;
+    ons = (a.Pb ? a.Pb[b] : a.P) - bb / (real)n;
   }
   real zn = 0;
   if (tid < kRow2Rows && r < n) {
@@ -1907,6 +1911,11 @@ struct sa_ctx {
   int beta2_cap = 0;
   double P = 0;
   bool power_set = false;
+  // per-codeword power allocation (sa_stage_power_batch): c [Bcap][L], P [Bcap]
+  void* d_cb = nullptr;
+  void* d_Pb = nullptr;
+  bool pb_on = false;
+  bool shared_power = false;  // sa_stage's Pl staged (c_l of the binary64 glue kernels)
   size_t bytes = 0;
   std::map<std::tuple<int, int, int, int>, hipGraphExec_t> graphs;
   int last_B = 0, last_T = 0;
@@ -1938,7 +1947,7 @@ void drop_graphs(sa_ctx* c) {
 
 void free_workspace(sa_ctx* c) {
   void** bufs[] = {&c->d_y, &c->d_z, &c->d_beta, &c->d_out, &c->d_abp, &c->d_bbp,
-                   &c->d_zzp, &c->d_tau, &c->d_azp};
+                   &c->d_zzp, &c->d_tau, &c->d_azp, &c->d_cb, &c->d_Pb};
   for (void** p : bufs) {
     dev_free(*p);
     *p = nullptr;
@@ -1948,6 +1957,10 @@ void free_workspace(sa_ctx* c) {
   dev_free(c->d_beta2); c->d_beta2 = nullptr;
   c->beta2_cap = 0;
   c->Bcap = c->Tcap = 0;
+  if (c->pb_on) {  // the per-codeword powers went with the workspace
+    c->pb_on = false;
+    c->power_set = c->shared_power;
+  }
 }
 
 int ensure_workspace(sa_ctx* c, int B, int T) {
@@ -1972,6 +1985,8 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   if ((rc = dev_alloc(c, &c->d_tau, (size_t)nB * (nT + 1) * s))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_iters, (size_t)nB * sizeof(int)))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_idx, (size_t)nB * c->L * sizeof(int32_t)))) return rc;
+  if ((rc = dev_alloc(c, &c->d_cb, (size_t)nB * c->L * s))) return rc;
+  if ((rc = dev_alloc(c, &c->d_Pb, (size_t)nB * s))) return rc;
   if (c->backend == SA_BACKEND_DENSE)
     if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->RS * c->lda * sizeof(float)))) return rc;
   c->Bcap = nB;
@@ -2043,6 +2058,8 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   a.T1 = c->Tcap + 1; a.t = t; a.mode = mode; a.early_stop = early_stop;
   a.RS = 1;
   a.B = 0; a.NC = 0;
+  a.cst = c->pb_on ? c->L : 0;
+  if (c->pb_on) a.c = (const real*)c->d_cb;
   a.sqrt_n = (real)std::sqrt((double)c->n);
   return a;
 }
@@ -2059,6 +2076,7 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb
   // the dense matrix already carries the 1/sqrt(n) of sparc_ldpc.py:143-146
   a.sqrt_n = c->backend == SA_BACKEND_DENSE ? (real)1 : (real)std::sqrt((double)c->n);
   a.P = (real)c->P;
+  a.Pb = c->pb_on ? (const real*)c->d_Pb : nullptr;
   return a;
 }
 
@@ -2371,7 +2389,8 @@ int run_graph(sa_ctx* c, int B, int T, int flags, int has_b0) {
     c->last_T = T;
     return SA_OK;
   }
-  const auto key = std::make_tuple(B, T, flags, has_b0);
+  // the power-allocation mode selects the captured kernel arguments (c, P arrays)
+  const auto key = std::make_tuple(B, T, flags | (c->pb_on ? 0x10000 : 0), has_b0);
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
@@ -2418,6 +2437,38 @@ int set_power(sa_ctx* c, const double* Pl) {
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(c->d_cd, cl.data(), (size_t)c->L * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));  // cl is a host temporary
+  c->pb_on = false;  // back to one allocation (graphs are keyed on the mode)
+  c->shared_power = true;
+  c->power_set = true;
+  return SA_OK;
+}
+
+// Per-codeword power allocations Pl [B][L] for the next runs of B' <= B
+// codewords (c_{b,l} = sqrt(n Pl_{b,l}), P_b = sum_l Pl_{b,l}).  A section with
+// Pl = 0 has c = 0, so its estimate stays exactly 0 (beta = c e / S) and it
+// adds nothing to A beta or to sum(beta^2): AMP over the remaining sections
+// with the same n, i.e. the reference's sparc_transforms_shorter decode
+// (amp_exit.py:113-116) as a mask, per codeword, in one batch.
+int set_power_batch(sa_ctx* c, int B, const double* Pl) {
+  if (!Pl) return fail(SA_ERR_ARG, "Pl is NULL");
+  if (c->backend == SA_BACKEND_DENSE) return fail(SA_ERR_UNSUPPORTED, "per-codeword power: Hadamard backend only");
+  const size_t L = (size_t)c->L;
+  std::vector<double> cb((size_t)B * L), Pb(B);
+  for (int b = 0; b < B; ++b) {
+    double P = 0;
+    for (size_t l = 0; l < L; ++l) {
+      const double p = Pl[(size_t)b * L + l];
+      if (!(p >= 0)) return fail(SA_ERR_ARG, "Pl must be non-negative");
+      cb[(size_t)b * L + l] = std::sqrt((double)c->n * p);
+      P += p;
+    }
+    Pb[b] = P;
+  }
+  int rc = upload(c, c->d_cb, cb.data(), (size_t)B * L);
+  if (!rc) rc = upload(c, c->d_Pb, Pb.data(), (size_t)B);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->pb_on = true;
   c->power_set = true;
   return SA_OK;
 }
@@ -2963,6 +3014,15 @@ int sa_stage(sa_ctx* c, int B, const double* y, const double* Pl, const double* 
   if (y && (rc = upload(c, c->d_y, y, (size_t)B * c->n))) return rc;  // NULL: keep the staged y
   if (beta0 && (rc = upload(c, c->d_beta, beta0, (size_t)B * c->L * c->M))) return rc;
   return SA_OK;
+}
+
+int sa_stage_power_batch(sa_ctx* c, int B, const double* Pl) {
+  if (check_ctx(c)) return SA_ERR_ARG;
+  if (B <= 0) return fail(SA_ERR_ARG, "sa_stage_power_batch: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
+  if (rc) return rc;
+  return set_power_batch(c, B, Pl);
 }
 
 int sa_run(sa_ctx* c, int B, int T, int flags) {

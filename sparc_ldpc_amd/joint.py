@@ -11,6 +11,12 @@ batched:
   BP -> bp2sp -> AMP re-initialised with the soft LDPC output.
 * ``hard`` — ``hardinitbeta_amp_ldpc_sim`` (:715-860): AMP, BP, AMP
   re-initialised with the one-hot hard decisions.
+* ``threshold`` — ``soft_amp_ldpc_hardinit`` (:862-1047): AMP, then rounds of
+  BP -> threshold decisions (amp_exit.hard_initialisation) -> cancel the
+  decided sections from y -> AMP over the undecided ones.  Batched, each
+  codeword has its own undecided set: the shortened operator of the reference
+  becomes a per-codeword section mask (sections with Pl = 0,
+  ``SparcOperator.stage_power_batch``) on one full-size operator.
 
 Every step of a round runs on the device: encoding (``sa_encode``), AMP
 (``sa_run``), the section->bit LLRs (``sa_llr``), belief propagation
@@ -35,7 +41,7 @@ from .operators import SparcOperator, make_ordering
 __all__ = ["JointDecoder", "joint_decoder", "draw_reps", "amp_ldpc_sim_ldpc", "soft_amp_ldpc_sim",
            "hardinitbeta_amp_ldpc_sim", "sim_ldpc", "waterfall", "sp2bp", "bp2sp", "mc_joint"]
 
-MODES = ("originalHard", "soft", "hard")
+MODES = ("originalHard", "soft", "hard", "threshold")
 
 
 def sp2bp(beta, L, M):
@@ -110,6 +116,7 @@ class JointDecoder:
         self.sub = self.op.subset(np.arange(self.l0)) if self.l0 > 0 else None
         self.total_bits = self.L * self.logm
         self.R = (self.L * self.logm - (code.N - code.K)) / n  # sparc_ldpc.py:541
+        self._masked = None  # full-size operator for the per-codeword masked decodes (threshold mode)
 
     # -- message / channel draws (the reference's order) --------------------------
     def draw(self, rs, B, sigma):
@@ -122,7 +129,7 @@ class JointDecoder:
         self.code.run_buffers(B, dectype)
         return d_app
 
-    def run(self, idx, noise, Pl, mode="soft", soft_iter=2):
+    def run(self, idx, noise, Pl, mode="soft", soft_iter=2, threshold=0.5):
         """Decode B codewords (section indices idx (B, L), noise (B, n)).
 
         Returns dict of per-rep bit-error COUNTS: 'amp' (B, rounds), 'ldpc'
@@ -131,7 +138,7 @@ class JointDecoder:
             raise ValueError(f"mode must be one of {MODES}")
         idx = np.ascontiguousarray(idx, dtype=np.int32)
         self.stage(idx, noise, Pl)
-        return self.decode_staged(idx, Pl, mode, soft_iter)
+        return self.decode_staged(idx, Pl, mode, soft_iter, threshold)
 
     def stage(self, idx, noise, Pl):
         """Encode on the device: y = A beta(idx) + noise becomes the staged input."""
@@ -144,7 +151,7 @@ class JointDecoder:
         self.op.encode(idx, noise)
         self.code.device_buffers(B)
 
-    def decode_staged(self, idx, Pl, mode="soft", soft_iter=2):
+    def decode_staged(self, idx, Pl, mode="soft", soft_iter=2, threshold=0.5):
         """The joint decode of the staged batch (see run); idx only scores the decisions."""
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
@@ -185,6 +192,8 @@ class JointDecoder:
                 op.wait()
                 rx = op.decide(B)
                 errs_amp.append(self._errs(idx, rx))
+        elif mode == "threshold":
+            self._threshold_rounds(B, idx, Pl, soft_iter, threshold, errs_amp, errs_ldpc, bp_iters)
         else:  # hard
             d_app = self._bp(B)
             bp_iters.append(self.code.fetch_buffers(B, app=False)[1])
@@ -200,6 +209,44 @@ class JointDecoder:
         out["ldpc"] = np.stack(errs_ldpc, axis=1) if errs_ldpc else np.zeros((B, 0), dtype=np.int64)
         out["bp_iters"] = np.stack(bp_iters, axis=1) if bp_iters else np.zeros((B, 0), dtype=np.int64)
         return out
+
+    def _threshold_rounds(self, B, idx, Pl, soft_iter, threshold, errs_amp, errs_ldpc, bp_iters):
+        """The information-exchange rounds of soft_amp_ldpc_hardinit
+        (sparc_ldpc.py:960-1041) for the batch; the first AMP has run on self.op."""
+        op, T, L, logm, l0, ns = self.op, self.T, self.L, self.logm, self.l0, self.ns
+        LLR = op.llr(B, 0, L)  # :960-970, every section
+        if self._masked is None:
+            self._masked = op.subset(np.arange(L))
+        mk = self._masked
+        mk.reserve(B, T)
+        mk.stage_power(B, Pl)  # c_l of the LLR kernel
+        for i in range(soft_iter):
+            app, it = self.code.decode_batch(LLR[:, l0 * logm:])  # :973
+            bp_iters.append(it)
+            LLR[:, l0 * logm:] = app
+            errs_ldpc.append(self._llr_errs(idx, LLR))  # :977
+            if i == soft_iter - 1:
+                break
+            dec = op.threshold(B, l0, ns, app, threshold)  # :984-999 + amp_exit.py:56-105
+            full = np.full((B, L), -1, dtype=np.int32)
+            full[:, l0:] = dec
+            undecided = full < 0
+            if undecided.any():  # :1006-1032, each codeword over its own undecided sections
+                op.cancel(full, mk)  # y - A beta(decided)
+                mk.stage_power_batch(B, np.where(undecided, np.asarray(Pl, np.float64)[None, :], 0.0))
+                mk.run(B, T)
+                mk.wait()
+                llr = mk.llr(B, 0, L).reshape(B, L, logm)
+                LLR.reshape(B, L, logm)[undecided] = llr[undecided]
+            errs_amp.append(self._llr_errs(idx, LLR))  # :1038
+
+    def _llr_errs(self, idx, LLR):
+        """Bit errors of the hard decisions of LLR against the section indices
+        (ber_from_LLRs, sparc_ldpc.py:343-356, times the bit count)."""
+        B = idx.shape[0]
+        bits = (np.asarray(LLR) < 0.0).astype(np.int64).reshape(B, self.L, self.logm)
+        hat = (bits * (1 << np.arange(self.logm - 1, -1, -1))).sum(axis=2)
+        return self._errs(idx, hat)
 
     def _errs(self, a, b):
         from .harness import _popcount
@@ -274,7 +321,7 @@ def hardinitbeta_amp_ldpc_sim(sparcparams: SPARCParams, ldpcparams: LDPCParams, 
     return [float(e) / tb for e in r["amp"][0]], [float(e) / tb for e in r["ldpc"][0]], jd.R
 
 
-def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256):
+def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256, threshold=0.5):
     """Seeded batched reps: rep s draws from RandomState(s) in the reference's
     order.  Returns the per-rep error-count dict of JointDecoder.run, in seed order."""
     seeds = list(seeds)
@@ -282,7 +329,7 @@ def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256):
     for s0 in range(0, len(seeds), batch):
         chunk = seeds[s0:s0 + batch]
         idx, noise = jd.draw([np.random.RandomState(s) for s in chunk], len(chunk), sigma)
-        parts.append(jd.run(idx, noise, Pl, mode, soft_iter))
+        parts.append(jd.run(idx, noise, Pl, mode, soft_iter, threshold))
     return {k: np.concatenate([p[k] for p in parts], axis=0) for k in parts[0]}
 
 

@@ -246,6 +246,15 @@ class SparcOperator:
         assert Pl.size == self.L, "Pl must hold L section powers"
         check(self._lib.sa_stage(self._ctx, int(B), None, dptr(Pl), None))
 
+    def stage_power_batch(self, B, Pl):
+        """Stage per-codeword section powers Pl (B, L) for the next run of up to B
+        codewords; Pl = 0 drops a section (β stays 0: the shortened-operator decode
+        of sparc_transforms_shorter as a per-codeword mask).  stage_power returns
+        to one allocation."""
+        Pl = as_f64(Pl)
+        assert Pl.shape == (B, self.L), "Pl must be (B, L)"
+        check(self._lib.sa_stage_power_batch(self._ctx, int(B), dptr(Pl)))
+
     def encode(self, idx, noise=None):
         """Stage y = A β(idx) + noise (sparc_ldpc.py:436-446); idx (B, L) section indices."""
         idx = np.ascontiguousarray(idx, dtype=np.int32)

@@ -22,7 +22,9 @@ from .harness import SPARCParams, LDPCParams, pa_parameterised, _popcount
 from .operators import AbOp, SparcOperator, make_ordering, sparc_transforms_shorter
 
 __all__ = ["J", "J_inverse", "gen_bits", "hard_initialisation", "prep_y", "remove_common_zeros", "calc_E",
-           "hist_E", "calc_I_e", "polynomial", "soft_amp_ldpc_hardinit", "ber_from_LLRs"]
+           "hist_E", "calc_I_e", "polynomial", "soft_amp_ldpc_hardinit", "ber_from_LLRs", "soft_hardinit_plot"]
+
+_RLDPC = {"5/6": 5 / 6, "1/2": 1 / 2, "0.45": 0.45, "3/8": 3 / 8}  # sparc_ldpc.py:1458-1467
 
 
 # ---- J-function approximations (amp_exit.py:28-46) ----------------------------------
@@ -264,3 +266,93 @@ def soft_amp_ldpc_hardinit(sparcparams: SPARCParams, ldpcparams: LDPCParams, sof
         ber_amp.append(ber_from_LLRs(M, LLR, idx, total_bits))
     R = (L * logm - (nl - kl)) / n
     return ber_amp, ber_ldpc, R
+
+
+def soft_hardinit_plot(sparcparams: SPARCParams, ldpcparams: LDPCParams, csv_filename=None, png_filename=None,
+                       sections=None, datapoints=10, MIN_ERRORS=100, MAX_BLOCKS=500, soft_iter=3, threshold=0.6,
+                       batch=64, seed0=0, precision="fp64", rank=0, world=1, allreduce=None, sigmas=None):
+    """The threshold-initialised exchange sweep of sparc_ldpc.py:1435-1590 on the GPU.
+
+    Per sigma of linspace(0.9, 1.4, datapoints) (:1488): blocks of
+    soft_amp_ldpc_hardinit at r_sparc and of plain SPARC at the same overall
+    rate R = (L log2 M - nl (1 - R_ldpc)) / n (:1480-1481), until MIN_ERRORS
+    PLAIN block errors or MAX_BLOCKS blocks (:1503-1524); BER columns are
+    means over the blocks; Eb/N0 = 20 log10(p / (2 R sigma^2)) (:1533-1535).
+    IEEE 802.11n / 802.16 codes share the seed-0 design, so blocks run
+    ``batch`` at a time from seeded RandomStates (JointDecoder mode
+    "threshold": per-codeword section masks), sharded over ranks like
+    joint.waterfall; the designed protographs draw a fresh random design per
+    block in the reference (:916-922), so those blocks run one at a time
+    (soft_amp_ldpc_hardinit, global np.random).  Returns the rows
+    (EbN0_dB, BER_amp [soft_iter], BER_ldpc [soft_iter], BER_plain, blocks,
+    block_errors); rank 0 appends the reference's CSV (:1537-1542).
+    No plots (figure code is out of scope)."""
+    from .harness import mc_decode, amp_ldpc_sim
+    from .joint import joint_decoder, mc_joint, _ber_point_multi
+    L, M = sparcparams.L, sparcparams.M
+    logm = int(np.log2(M))
+    p, r_sparc, T = sparcparams.p, sparcparams.r, sparcparams.t
+    if ldpcparams.r_ldpc not in _RLDPC:
+        raise ValueError("Invalid choice of ldpc rate, please choose a different one.")
+    Rldpc = _RLDPC[ldpcparams.r_ldpc]
+    if sections is None:
+        sections = L
+    nl = logm * sections
+    z = ldpcparams.z
+    std = ldpcparams.standard in ("802.11n", "802.16")
+    if z is None:
+        z = int(nl / 24) if std else int(nl / 40)
+    ldp = LDPCParams(ldpcparams.standard, ldpcparams.r_ldpc, z, ldpcparams.ptype)
+    n_f = L * logm / r_sparc
+    R = (L * logm - nl * (1 - Rldpc)) / n_f
+    SIGMA = np.linspace(0.9, 1.4, datapoints) if sigmas is None else np.asarray(sigmas, dtype=np.float64)
+    n = int(L * np.log2(M) / r_sparc)
+    n_plain = int(L * np.log2(M) / R)
+    total_bits = L * logm
+    Pl = p / L * np.ones(L)
+    rows = []
+    if std:
+        jd = joint_decoder(L, M, n, ldp, T, precision=precision)
+        assert jd.ns == sections, "sections must match the LDPC code length"
+        plain = SparcOperator(L, M, n_plain, make_ordering(L, M, n_plain, 0), None, precision)
+    for pi, sigma in enumerate(SIGMA):
+        sigma = float(sigma)
+        if std:
+            def round_fn(seeds, sigma=sigma):
+                rj = mc_joint(jd, Pl, sigma, seeds, "threshold", soft_iter, batch, threshold)
+                be_plain, _ = mc_decode(plain, Pl, sigma, T, [s + 5_000_000 for s in seeds], batch=batch)
+                return be_plain, np.concatenate([rj["amp"], rj["ldpc"]], axis=1)
+
+            res = _ber_point_multi(round_fn, total_bits, MIN_ERRORS, MAX_BLOCKS, batch, rank, world, allreduce,
+                                   seed0 + pi * 10_000_000)
+            cols = np.asarray(res["cols"])
+            ber_amp, ber_ldpc = cols[:soft_iter], cols[soft_iter:]
+            ber_plain, nblocks, nerr = res["BER"], res["blocks"], res["block_errors"]
+        else:
+            sp_c = SPARCParams(L, M, sigma, p, r_sparc, T)
+            sp_plain = SPARCParams(L, M, sigma, p, R, T)
+            cum_amp, cum_ldpc, cum_plain = np.zeros(soft_iter), np.zeros(soft_iter), 0.0
+            nerr = nblocks = 0
+            while nerr < MIN_ERRORS:
+                ba, bl, _ = soft_amp_ldpc_hardinit(sp_c, ldp, soft_iter, threshold, precision=precision)
+                bpl = amp_ldpc_sim(sp_plain)[0]
+                cum_amp += np.asarray(ba[:soft_iter])
+                cum_ldpc += np.asarray(bl[:soft_iter])
+                cum_plain += bpl
+                nerr += 1 if bpl else 0
+                nblocks += 1
+                if nblocks >= MAX_BLOCKS:
+                    break
+            ber_amp, ber_ldpc, ber_plain = cum_amp / nblocks, cum_ldpc / nblocks, cum_plain / nblocks
+        ebno_db = 20 * np.log10(1 / (2 * R) * (p / sigma ** 2))
+        rows.append(dict(EbN0_dB=float(ebno_db), sigma=sigma, BER_amp=[float(x) for x in ber_amp],
+                         BER_ldpc=[float(x) for x in ber_ldpc], BER_plain=float(ber_plain), blocks=int(nblocks),
+                         block_errors=int(nerr)))
+    if csv_filename and rank == 0:
+        with open(csv_filename, "a", newline="") as fh:
+            wr = csv.DictWriter(fh, fieldnames=["EbN0_dB", "BER_amp", "BER_ldpc", "BER_plain"])
+            wr.writeheader()
+            for r in rows:
+                wr.writerow({"EbN0_dB": r["EbN0_dB"], "BER_amp": np.array(r["BER_amp"]),
+                             "BER_ldpc": np.array(r["BER_ldpc"]), "BER_plain": r["BER_plain"]})
+    return rows

@@ -83,3 +83,78 @@ def test_hard_initialisation_dropin():
     v = rs.randn(Ls * M, 1)
     Ab_s, _ = sp.sparc_transforms_shorter(Ls, M, n, ordering[secs], precision="fp64")
     np.testing.assert_allclose(Ab_new(v), Ab_s(v), rtol=0, atol=1e-12)
+
+
+def test_hardinit_batched_matches_reference():
+    """The same reference reps decoded as ONE batch (JointDecoder mode
+    "threshold": every codeword's undecided sections as a per-codeword mask on
+    one full-size operator) instead of per-codeword shortened operators."""
+    import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd.joint import joint_decoder
+    g = golden("joint.npz")
+    L, M, P, r, T, z, sigma, thr = g["thr|cfg"]
+    L, M, T = int(L), int(M), int(T)
+    n = int(L * np.log2(M) / float(r))
+    keys = _keys("thr|hardinit|")
+    seeds = [int(k.split("|")[-1]) for k in keys]
+    jd = joint_decoder(L, M, n, sp.LDPCParams("802.16", "5/6", int(z)), T, precision="fp64")
+    idx, noise = jd.draw([np.random.RandomState(s) for s in seeds], len(seeds), float(sigma))
+    out = jd.run(idx, noise, float(P) / L * np.ones(L), "threshold", 3, float(thr))
+    tb = jd.total_bits
+    for i, key in enumerate(keys):
+        assert np.array_equal(idx[i], g[key + "|idx"].astype(np.int32))
+        got = np.concatenate([out["amp"][i], out["ldpc"][i]]) / tb
+        ref = g[key + "|ber"]
+        assert got.shape == ref.shape and got[0] == ref[0]
+        its = [int(g[key + f"|it{k}"][0]) for k in range(3) if key + f"|it{k}" in g]
+        if all(it < 200 for it in its):
+            np.testing.assert_array_equal(got, ref)
+        else:
+            assert np.max(np.abs(got - ref)) <= 0.03
+
+
+@pytest.mark.parametrize("L,M,n,B", [(64, 32, 320, 5), (64, 32, 320, 2), (256, 256, 2048, 1)])
+def test_power_batch_mask_equals_shortened_operator(L, M, n, B):
+    """Pl = 0 sections of a per-codeword power allocation = the reference's
+    sparc_transforms_shorter decode over the other sections (fp64, different
+    summation grouping only); equal rows reproduce the shared allocation
+    bit for bit.  Batched (k_secb), unbatched (k_sec) and k_sec4 paths."""
+    import sparc_ldpc_amd as sp
+    T = 16
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp64", device=0)
+    Pl = 4.0 / L * np.ones(L)
+    rs = np.random.RandomState(11)
+    idx = rs.randint(0, M, (B, L)).astype(np.int32)
+    op.reserve(B, T)
+    op.stage_power(B, Pl)
+    op.encode(idx, 0.4 * rs.randn(B, n))
+    op.run(B, T)
+    op.wait()
+    ref_shared, it_shared = op.fetch(B)
+    op.stage_power_batch(B, np.tile(Pl, (B, 1)))
+    op.run(B, T)
+    op.wait()
+    got, it = op.fetch(B)
+    assert np.array_equal(got, ref_shared) and np.array_equal(it, it_shared)
+    # masks: codeword b drops a different random subset of sections
+    masks = rs.rand(B, L) < 0.3
+    op.stage_power_batch(B, np.where(masks, 0.0, Pl[None, :]))
+    op.run(B, T)
+    op.wait()
+    got, it = op.fetch(B)
+    assert all(np.all(got[b].reshape(L, M)[masks[b]] == 0) for b in range(B))
+    # the masked decode equals AMP over the kept sections on the host operator
+    from oracle import amp_oracle as orc
+    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
+    rs2 = np.random.RandomState(11)
+    _ = rs2.randint(0, M, (B, L))
+    noise = 0.4 * rs2.randn(B, n)
+    c = np.sqrt(n * Pl)
+    for b in range(B):
+        beta0 = np.zeros((L * M, 1))
+        beta0[np.arange(L) * M + idx[b], 0] = c
+        yb = oAb(beta0) + noise[b].reshape(-1, 1)
+        keep = np.nonzero(~masks[b])[0]
+        sAb, sAz = orc.sparc_transforms_shorter(len(keep), M, n, oord[keep])
+        refb = orc.amp(yb, 0, Pl[keep], len(keep), M, T, sAb, sAz).reshape(len(keep), M)
+        np.testing.assert_allclose(got[b].reshape(L, M)[keep], refb, rtol=0, atol=1e-9 * np.abs(refb).max())

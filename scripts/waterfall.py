@@ -9,6 +9,10 @@
             (all 512 sections; originalHard: 384 as the shipped call), every
             BER column incl. plain SPARC and LDPC+BPSK, MIN_ERRORS=200 /
             MAX_BLOCKS=250.
+  threshold : soft_hardinit_plot() (sparc_ldpc.py:1435-1590): threshold-
+            initialised exchange, L=M=512 P=4 r_sparc=1 T=64 + 802.16 rate 5/6
+            over all 512 sections, soft_iter=2, sigma = linspace(0.9, 1.4, 10),
+            threshold 0.6 or 0.8 (--threshold), MIN_ERRORS = MAX_BLOCKS = 200.
   l768    : soft_hard_plot()'s BER_sparc column (sparc_ldpc.py:1285-1432):
             L=768 M=512 P=1.8 at the overall rate R=0.8765 (sec=569),
             sigma = linspace(0.8, 0.4, 10), 100 reps per point.
@@ -30,7 +34,10 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sweep", default="plain", choices=["plain", "l768", "soft", "hard", "originalHard"])
+    ap.add_argument("--sweep", default="plain", choices=["plain", "l768", "soft", "hard", "originalHard", "threshold"])
+    ap.add_argument("--threshold", type=float, default=0.6)
+    ap.add_argument("--unit-cancel", action="store_true",
+                    help="threshold sweep: cancel decided sections with amplitude 1 (the reference before its fix)")
     ap.add_argument("--points", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--out", default="gpurun_out/waterfall")
@@ -66,6 +73,19 @@ def main():
         ref = pub["waterfall_joint"]["runs"][args.sweep]
         for i, r in enumerate(rows):
             r["reference"] = {k: ref[k][i] for k in ref if k not in ("file", "EbN0_dB")}
+    elif args.sweep == "threshold":
+        cfg = pub["threshold_init"]["config"]
+        spp = sp.SPARCParams(cfg["L"], cfg["M"], None, cfg["P"], cfg["r_sparc"], cfg["T"])
+        lp = sp.LDPCParams(cfg["standard"], cfg["r_ldpc"], None)
+        sig = np.linspace(*cfg["sigma"])[:args.points]
+        rows = sp.soft_hardinit_plot(spp, lp, args.out + ".csv" if rank == 0 else None, None, cfg["sections"],
+                                     MIN_ERRORS=200, MAX_BLOCKS=200, soft_iter=cfg["soft_iter"],
+                                     threshold=args.threshold, batch=args.batch, precision=args.precision or "fp64",
+                                     rank=rank, world=world, allreduce=dist.allreduce_sum, sigmas=sig,
+                                     unit_cancel=args.unit_cancel)
+        refs = [r for r in pub["threshold_init"]["runs"] if r["threshold"] == args.threshold]
+        for i, r in enumerate(rows):
+            r["reference_runs"] = [{k: ref[k][i] for k in ("BER_amp", "BER_ldpc", "BER_plain")} for ref in refs]
     else:
         cfg = pub["soft_hard_BER_sparc"]["config"]
         L, M, P, T = cfg["L"], cfg["M"], cfg["P"], cfg["T"]

@@ -129,7 +129,7 @@ class JointDecoder:
         self.code.run_buffers(B, dectype)
         return d_app
 
-    def run(self, idx, noise, Pl, mode="soft", soft_iter=2, threshold=0.5):
+    def run(self, idx, noise, Pl, mode="soft", soft_iter=2, threshold=0.5, unit_cancel=False):
         """Decode B codewords (section indices idx (B, L), noise (B, n)).
 
         Returns dict of per-rep bit-error COUNTS: 'amp' (B, rounds), 'ldpc'
@@ -138,7 +138,7 @@ class JointDecoder:
             raise ValueError(f"mode must be one of {MODES}")
         idx = np.ascontiguousarray(idx, dtype=np.int32)
         self.stage(idx, noise, Pl)
-        return self.decode_staged(idx, Pl, mode, soft_iter, threshold)
+        return self.decode_staged(idx, Pl, mode, soft_iter, threshold, unit_cancel)
 
     def stage(self, idx, noise, Pl):
         """Encode on the device: y = A beta(idx) + noise becomes the staged input."""
@@ -150,9 +150,15 @@ class JointDecoder:
         self.op.stage_power(B, np.asarray(Pl, dtype=np.float64))
         self.op.encode(idx, noise)
         self.code.device_buffers(B)
+        self._noise = np.asarray(noise, dtype=np.float64).reshape(B, self.n)
 
-    def decode_staged(self, idx, Pl, mode="soft", soft_iter=2, threshold=0.5):
-        """The joint decode of the staged batch (see run); idx only scores the decisions."""
+    def decode_staged(self, idx, Pl, mode="soft", soft_iter=2, threshold=0.5, unit_cancel=False):
+        """The joint decode of the staged batch (see run); idx only scores the
+        decisions.  unit_cancel (threshold mode only): cancel decided sections
+        with amplitude 1 instead of sqrt(n Pl_l), the reference's behaviour
+        before the fix its comment at amp_exit.py:97-98 records, with which its
+        published threshold-init CSVs were evidently produced (see
+        DESIGN.md §10)."""
         if mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         idx = np.ascontiguousarray(idx, dtype=np.int32)
@@ -193,7 +199,7 @@ class JointDecoder:
                 rx = op.decide(B)
                 errs_amp.append(self._errs(idx, rx))
         elif mode == "threshold":
-            self._threshold_rounds(B, idx, Pl, soft_iter, threshold, errs_amp, errs_ldpc, bp_iters)
+            self._threshold_rounds(B, idx, Pl, soft_iter, threshold, errs_amp, errs_ldpc, bp_iters, unit_cancel)
         else:  # hard
             d_app = self._bp(B)
             bp_iters.append(self.code.fetch_buffers(B, app=False)[1])
@@ -210,7 +216,7 @@ class JointDecoder:
         out["bp_iters"] = np.stack(bp_iters, axis=1) if bp_iters else np.zeros((B, 0), dtype=np.int64)
         return out
 
-    def _threshold_rounds(self, B, idx, Pl, soft_iter, threshold, errs_amp, errs_ldpc, bp_iters):
+    def _threshold_rounds(self, B, idx, Pl, soft_iter, threshold, errs_amp, errs_ldpc, bp_iters, unit_cancel=False):
         """The information-exchange rounds of soft_amp_ldpc_hardinit
         (sparc_ldpc.py:960-1041) for the batch; the first AMP has run on self.op."""
         op, T, L, logm, l0, ns = self.op, self.T, self.L, self.logm, self.l0, self.ns
@@ -232,13 +238,29 @@ class JointDecoder:
             full[:, l0:] = dec
             undecided = full < 0
             if undecided.any():  # :1006-1032, each codeword over its own undecided sections
-                op.cancel(full, mk)  # y - A beta(decided)
+                if unit_cancel:
+                    self._stage_unit_cancel(B, idx, full, Pl, mk)
+                else:
+                    op.cancel(full, mk)  # y - A beta(decided)
                 mk.stage_power_batch(B, np.where(undecided, np.asarray(Pl, np.float64)[None, :], 0.0))
                 mk.run(B, T)
                 mk.wait()
                 llr = mk.llr(B, 0, L).reshape(B, L, logm)
                 LLR.reshape(B, L, logm)[undecided] = llr[undecided]
             errs_amp.append(self._llr_errs(idx, LLR))  # :1038
+
+    def _stage_unit_cancel(self, B, idx, full, Pl, mk):
+        """Stage y - A beta_1(decided) into mk, beta_1 one-hot with amplitude 1."""
+        L, M = self.L, self.M
+        c = np.sqrt(self.n * np.asarray(Pl, dtype=np.float64))
+        rows = np.arange(B)[:, None]
+        b0 = np.zeros((B, L * M))
+        b0[rows, np.arange(L)[None, :] * M + idx] = c[None, :]
+        y = self.op.Ab_batch(b0) + self._noise[:B]
+        b1 = np.zeros((B, L * M))
+        r, l = np.nonzero(full >= 0)
+        b1[r, l * M + full[r, l]] = 1.0
+        mk.stage(y - self.op.Ab_batch(b1), Pl)
 
     def _llr_errs(self, idx, LLR):
         """Bit errors of the hard decisions of LLR against the section indices
@@ -321,7 +343,7 @@ def hardinitbeta_amp_ldpc_sim(sparcparams: SPARCParams, ldpcparams: LDPCParams, 
     return [float(e) / tb for e in r["amp"][0]], [float(e) / tb for e in r["ldpc"][0]], jd.R
 
 
-def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256, threshold=0.5):
+def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256, threshold=0.5, unit_cancel=False):
     """Seeded batched reps: rep s draws from RandomState(s) in the reference's
     order.  Returns the per-rep error-count dict of JointDecoder.run, in seed order."""
     seeds = list(seeds)
@@ -329,7 +351,7 @@ def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256, t
     for s0 in range(0, len(seeds), batch):
         chunk = seeds[s0:s0 + batch]
         idx, noise = jd.draw([np.random.RandomState(s) for s in chunk], len(chunk), sigma)
-        parts.append(jd.run(idx, noise, Pl, mode, soft_iter, threshold))
+        parts.append(jd.run(idx, noise, Pl, mode, soft_iter, threshold, unit_cancel))
     return {k: np.concatenate([p[k] for p in parts], axis=0) for k in parts[0]}
 
 

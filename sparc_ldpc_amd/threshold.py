@@ -270,7 +270,8 @@ def soft_amp_ldpc_hardinit(sparcparams: SPARCParams, ldpcparams: LDPCParams, sof
 
 def soft_hardinit_plot(sparcparams: SPARCParams, ldpcparams: LDPCParams, csv_filename=None, png_filename=None,
                        sections=None, datapoints=10, MIN_ERRORS=100, MAX_BLOCKS=500, soft_iter=3, threshold=0.6,
-                       batch=64, seed0=0, precision="fp64", rank=0, world=1, allreduce=None, sigmas=None):
+                       batch=64, seed0=0, precision="fp64", rank=0, world=1, allreduce=None, sigmas=None,
+                       unit_cancel=False):
     """The threshold-initialised exchange sweep of sparc_ldpc.py:1435-1590 on the GPU.
 
     Per sigma of linspace(0.9, 1.4, datapoints) (:1488): blocks of
@@ -286,6 +287,9 @@ def soft_hardinit_plot(sparcparams: SPARCParams, ldpcparams: LDPCParams, csv_fil
     (soft_amp_ldpc_hardinit, global np.random).  Returns the rows
     (EbN0_dB, BER_amp [soft_iter], BER_ldpc [soft_iter], BER_plain, blocks,
     block_errors); rank 0 appends the reference's CSV (:1537-1542).
+    unit_cancel=True cancels decided sections with amplitude 1 (the
+    reference's behaviour before the fix noted at amp_exit.py:97-98, which its
+    published threshold-init CSVs reflect; batched path only).
     No plots (figure code is out of scope)."""
     from .harness import mc_decode, amp_ldpc_sim
     from .joint import joint_decoder, mc_joint, _ber_point_multi
@@ -319,7 +323,7 @@ def soft_hardinit_plot(sparcparams: SPARCParams, ldpcparams: LDPCParams, csv_fil
         sigma = float(sigma)
         if std:
             def round_fn(seeds, sigma=sigma):
-                rj = mc_joint(jd, Pl, sigma, seeds, "threshold", soft_iter, batch, threshold)
+                rj = mc_joint(jd, Pl, sigma, seeds, "threshold", soft_iter, batch, threshold, unit_cancel)
                 be_plain, _ = mc_decode(plain, Pl, sigma, T, [s + 5_000_000 for s in seeds], batch=batch)
                 return be_plain, np.concatenate([rj["amp"], rj["ldpc"]], axis=1)
 

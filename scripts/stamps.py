@@ -21,9 +21,13 @@ lib = sp.load_library()
 lib.sa_debug_stamps.argtypes = [ct.POINTER(ct.c_ulonglong)]
 # stamp order in time (index 10: after an explicit wait for every global load
 # issued so far, i.e. the bucket-table / previous-beta / Ab-table loads)
-order = [0, 1, 2, 10, 3, 4, 5, 6, 7, 8, 9]
-names = ["tau+loads", "z->LDS+bar", "wait tables", "gather", "fwht1", "denoise", "fwht2", "ts+bar", "rows",
-         "drain"]
+if op.plan(B)["section_kernel"] == "k_secb":
+    order = [0, 1, 2, 3, 4, 5, 6, 7]
+    names = ["loads+tau", "z->LDS+bar", "gather", "fwht+denoise+fwht", "T->LDS+bar", "rows", "drain"]
+else:
+    order = [0, 1, 2, 10, 3, 4, 5, 6, 7, 8, 9]
+    names = ["tau+loads", "z->LDS+bar", "wait tables", "gather", "fwht1", "denoise", "fwht2", "ts+bar", "rows",
+             "drain"]
 acc = np.zeros(len(order) - 1)
 for rep in range(20):
     op.run(B, T, early_stop=False); op.wait()

@@ -1167,13 +1167,15 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 }
 
 template <typename real, int E, int CB, int W>
-__global__ void __launch_bounds__(W * 64) k_secb(SecArgs<real> a) {
+__global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = W * 64;
   constexpr int NQ = (E + 3) / 4;
-  constexpr int KH = (E >= 16 || CB >= 4) ? 2 : 4;  // bucket h-steps with table loads in flight together
-  constexpr int KR = CB >= 4 ? 2 : 3;   // rows per thread whose Ab-table loads are in flight together
-  constexpr bool PB = CB <= 2;          // prefetch the previous beta with the first loads
+  // binary64: fewer loads in flight so a wave fits 128 VGPRs (two workgroups per CU)
+  constexpr bool F64 = sizeof(real) == 8;
+  constexpr int KH = (E >= 16 || CB >= 4 || F64) ? 2 : 4;  // bucket h-steps with table loads in flight together
+  constexpr int KR = (CB >= 4 || F64) ? 2 : 3;   // rows per thread whose Ab-table loads are in flight together
+  constexpr bool PB = CB <= 2 && !F64;           // prefetch the previous beta with the first loads
   constexpr int W4 = W / 4;             // 4-section table groups per workgroup
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int M = a.M, n = a.n;

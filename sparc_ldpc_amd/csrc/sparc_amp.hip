@@ -66,6 +66,17 @@ __device__ __forceinline__ float4 ld_stream(const float* p) {
 }
 
 
+// Load of a uniform value as a VECTOR load (opaque zero lane offset): a scalar
+// load's lgkmcnt wait would also wait for it at the next use of any other
+// scalar (SMEM returns out of order), serialising a memory round trip in
+// front of the kernel's other loads.
+template <typename T>
+__device__ __forceinline__ T ld_vmem(const T* p) {
+  int z0;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z0));
+  return p[z0];
+}
+
 // Store of a partial another kernel reads after the boundary (Ab partials):
 // non-temporal, so no dirty L2 line is left for the kernel-end writeback to
 // drain (c2: k_sec4 7.85 -> 7.65 us, +1.5 % codewords/s; c3 neutral).
@@ -207,11 +218,23 @@ template <> __device__ __forceinline__ double neg_inf<double>() { return -INFINI
 // partials i, i+64, ... in order, then a fixed xor-butterfly.  Every wave
 // that evaluates it (in any workgroup) gets the same bits, and all loads of
 // a lane are independent, so the latency is one round trip, not cnt.
+// (Loads are unconditional with a clamped index and issued four at a time
+// before the adds: a conditional load with its add sunk into the branch makes
+// the compiler wait for each load on the spot, one round trip per partial.)
 template <typename real>
 __device__ __forceinline__ real wave_sum_parts(const real* p, int cnt) {
   const int lane = threadIdx.x & 63;
   real s = 0;
-  for (int i = lane; i < cnt; i += 64) s += p[i];
+  for (int i0 = lane; i0 < cnt; i0 += 256) {
+    real t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 64 * u;
+      t[u] = p[i < cnt ? i : i0];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += i0 + 64 * u < cnt ? t[u] : (real)0;
+  }
   return wave_sum(s);
 }
 
@@ -227,21 +250,26 @@ __device__ __forceinline__ real wave_sum_pair(real a, real b) {
 
 // The z^2 partials for tau, loaded ahead of everything else a kernel needs
 // (vmcnt retires loads in order: tau then waits for these alone).  Same sum
-// as wave_sum_parts for NZ <= 64 * kZZ.
-constexpr int kZZ = 4;
-template <typename real>
+// as wave_sum_parts for NZ <= 64 * K.  The loads are unconditional (clamped
+// index, masked in tau()): with `cond ? p[i] : 0` the compiler sank the first
+// add into the branch and waited for that load before issuing anything else.
+template <typename real, int K = 4>
 struct ZZParts {
-  real v[kZZ];
+  real v[K];
   __device__ __forceinline__ void issue(const real* p, int cnt, int lane) {
 #pragma unroll
-    for (int q = 0; q < kZZ; ++q) v[q] = lane + 64 * q < cnt ? p[lane + 64 * q] : (real)0;
+    for (int q = 0; q < K; ++q) {
+      const int i = lane + 64 * q;
+      v[q] = p[i < cnt ? i : 0];
+    }
   }
   __device__ __forceinline__ real tau(const real* p, int cnt, int n) const {
+    const int lane = threadIdx.x & 63;
     real s;
-    if (cnt <= 64 * kZZ) {
+    if (cnt <= 64 * K) {
       s = 0;
 #pragma unroll
-      for (int q = 0; q < kZZ; ++q) s += v[q];
+      for (int q = 0; q < K; ++q) s += lane + 64 * q < cnt ? v[q] : (real)0;
       s = wave_sum(s);
     } else {
       s = wave_sum_parts(p, cnt);
@@ -541,7 +569,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     zst.issue(zb, n, tid);
     load_buckets<E, KH>(il, 0, a.nhi, M, lane, tb);
     if (a.mode == SEC_AMP) load_section<real, E>(bl, bprev, lane, M);
-    const real cl = a.c[(size_t)b * a.cst + lc];
+    const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
     if (a.mode == SEC_AMP) {
 #pragma unroll
       for (int u = 0; u < KR; ++u) {
@@ -552,7 +580,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     real tau2 = 1;
     if (a.mode == SEC_AMP) {
       const real tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, n);
-      const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+      const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
       const bool stop = a.early_stop && (tau == last);
       if (blockIdx.x == 0 && tid == 0) {
         a.tau[(size_t)b * a.T1 + a.t] = tau;
@@ -728,13 +756,13 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
   const real* zzb = a.zzp + (size_t)b * a.NZ;
   ZZParts<real> zz;
   zz.issue(zzb, a.NZ, lane);
-  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+  const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   const real* zb = a.z + (size_t)b * n;
   ZStage<real> zst;
   zst.issue(zb, n, tid);
   load_buckets<E2, KH>(il, 0, a.nhi, M, lane, tb);
   load_section<real, E2>(bl, bprev, lane, Mh);
-  const real cl = a.c[(size_t)b * a.cst + lc];
+  const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
   const int nk = min(KR, (n + 255) / 256);  // passes of 256 rows in the first chunk
 #pragma unroll
   for (int u = 0; u < KR; ++u) {
@@ -935,13 +963,13 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   const real* zzb = a.zzp + (size_t)b * a.NZ;
   ZZParts<real> zz;
   zz.issue(zzb, a.NZ, lane);
-  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+  const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   const real* zb = a.z + (size_t)b * n;
   ZStage<real, NT> zst;
   zst.issue(zb, n, tid);
   load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
   load_section<real, EQ>(bl, bprev, lane, Mq);
-  const real cl = a.c[(size_t)b * a.cst + lc];
+  const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
   const int nk = min(KR, (n + NT - 1) / NT);
 #pragma unroll
   for (int u = 0; u < KR; ++u) {
@@ -1217,6 +1245,10 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   real* bbw = zs + region;                   // [W][CB]
 
   // ---- every load independent of z in flight together ---------------------
+  // the z^2 partials of the CB codewords first: tau waits for these alone
+  ZZParts<real, F64 ? 2 : 3> zzc[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) zzc[c].issue(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, lane);
   // z rows of the CB codewords (first pass of the staging loop)
   constexpr int KZ = 4;
   real zr[KZ][CB];
@@ -1241,7 +1273,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   }
   real cl[CB];
 #pragma unroll
-  for (int c = 0; c < CB; ++c) cl[c] = a.c[(size_t)bc[c] * a.cst + lc];
+  for (int c = 0; c < CB; ++c) cl[c] = ld_vmem(a.c + (size_t)bc[c] * a.cst + lc);
   const ushort4* fw = a.fwd + (size_t)g * W4 * n;
   ushort4 f[KR][W4];
 #pragma unroll
@@ -1256,8 +1288,8 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   real tau2[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
-    const real tau = tau_from_parts(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
-    const real last = a.t > 0 ? a.tau[(size_t)bc[c] * a.T1 + a.t - 1] : (real)0;
+    const real tau = zzc[c].tau(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
+    const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
     const bool stop = a.early_stop && (tau == last);
     if (valid[c] && g == 0 && tid == 0) {
       a.tau[(size_t)bc[c] * a.T1 + a.t] = tau;
@@ -1454,12 +1486,13 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = blockIdx.x * kRowsPerBlk + lane;
   const int n = a.n;
-  real tau2 = 1;
+  // tau_t and tau_{t-1} are loaded with everything else; the early-stop
+  // test waits for them only after the Ab-partial loads are in flight
+  // (testing first cost a whole memory round trip per launch)
+  real tau = 1, last = 0;
   if (a.mode == ROW_AMP) {
-    const real tau = a.tau[(size_t)b * a.T1 + a.t];
-    const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
-    if (a.early_stop && tau == last) return;
-    tau2 = tau * tau;
+    tau = ld_vmem(a.tau + (size_t)b * a.T1 + a.t);
+    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   }
   // wave 0 finishes the rows: its operands that do not depend on the Ab
   // partials (y, z, the beta^2 partials) are loaded up front, in the same
@@ -1491,6 +1524,8 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
     }
     red[wv][lane] = acc;
   }
+  if (a.mode == ROW_AMP && a.early_stop && tau == last) return;  // uniform over the workgroup
+  const real tau2 = tau * tau;
   __syncthreads();
   if (wv != 0) return;
   real ons = 0;
@@ -1534,12 +1569,13 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
   const int rl = tid & (kRow2Rows - 1), pg = tid >> 5;
   const int r = blockIdx.x * kRow2Rows + rl;
   const int n = a.n;
-  real tau2 = 1;
+  // tau_t and tau_{t-1} are loaded with everything else; the early-stop
+  // test waits for them only after the Ab-partial loads are in flight
+  // (testing first cost a whole memory round trip per launch)
+  real tau = 1, last = 0;
   if (a.mode == ROW_AMP) {
-    const real tau = a.tau[(size_t)b * a.T1 + a.t];
-    const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
-    if (a.early_stop && tau == last) return;
-    tau2 = tau * tau;
+    tau = ld_vmem(a.tau + (size_t)b * a.T1 + a.t);
+    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   }
   const size_t o = (size_t)b * n + (r < n ? r : 0);
   real yv = 0, zv = 0, bbv[4] = {0, 0, 0, 0};
@@ -1569,6 +1605,8 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
     }
     red[pg][rl] = acc;
   }
+  if (a.mode == ROW_AMP && a.early_stop && tau == last) return;  // uniform over the workgroup
+  const real tau2 = tau * tau;
   __syncthreads();
   if (tid >= 64) return;
   real ons = 0;

@@ -36,6 +36,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sweep", default="plain", choices=["plain", "l768", "soft", "hard", "originalHard", "threshold"])
     ap.add_argument("--threshold", type=float, default=0.6)
+    ap.add_argument("--reps", type=int, default=0,
+                    help="l768: reps per sigma point (default: the published 100; BASELINE configs[3] is 1000 x 10)")
     ap.add_argument("--unit-cancel", action="store_true",
                     help="threshold sweep: cancel decided sections with amplitude 1 (the reference before its fix)")
     ap.add_argument("--points", type=int, default=10)
@@ -97,8 +99,9 @@ def main():
         Pl = P / L * np.ones(L)
         rows = []
         for i, sigma in enumerate(np.linspace(0.8, 0.4, 10)[:args.points]):
-            reps = cfg["reps_per_point"]
+            reps = args.reps or cfg["reps_per_point"]
             seeds = [j for j in range(i * 100000, i * 100000 + reps) if j % world == rank]
+            assert reps <= 100000
             be, it = sp.mc_decode(op, Pl, sigma, T, seeds, batch=args.batch)
             tot = dist.allreduce_sum(np.array([be.sum(), len(seeds), it.sum()], dtype=np.int64))
             ebno_db = 20 * np.log10(1 / (2 * R) * (P / sigma ** 2))  # sparc_ldpc.py:1414-1416

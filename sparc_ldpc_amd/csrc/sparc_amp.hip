@@ -109,9 +109,12 @@ __device__ __forceinline__ int xor_lane_i32(int x) {
   } else if constexpr (m == 2) {
     return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
   } else if constexpr (m == 4 || m == 8) {
-    const int up = __builtin_amdgcn_mov_dpp(x, 0x100 + m, 0xF, 0xF, false);  // row_shl:m  (lane + m)
-    const int dn = __builtin_amdgcn_mov_dpp(x, 0x110 + m, 0xF, 0xF, false);  // row_shr:m  (lane - m)
-    return (threadIdx.x & m) ? dn : up;
+    // two bank-masked DPP moves, no select: the banks (4-lane groups of a
+    // 16-lane row) whose lane bit m is set take row_shr:m (lane - m), the
+    // others row_shl:m (lane + m); every source lane stays inside its row
+    constexpr int hi = m == 4 ? 0xA : 0xC, lo = m == 4 ? 0x5 : 0x3;
+    const int dn = __builtin_amdgcn_update_dpp(x, x, 0x110 + m, 0xF, hi, false);
+    return __builtin_amdgcn_update_dpp(dn, x, 0x100 + m, 0xF, lo, false);
   } else if constexpr (m == 16) {
     const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
     return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
@@ -139,10 +142,23 @@ __device__ __forceinline__ real xor_lane(real x) {
 template <int m, typename real, int E>
 __device__ __forceinline__ void lane_butterfly(real (&x)[E], int lane) {
   const real sg = (lane & m) ? (real)-1 : (real)1;
+  if constexpr ((m == 16 || m == 32) && sizeof(real) == 4) {
+    // v_permlane{16,32}_swap of x with itself leaves a = the lower partner
+    // and b = the upper one in every lane: lower lanes a + b, upper a - b
+    // (the same two operands and rounding as fma(x, sg, partner))
 #pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const real p = xor_lane<m>(x[i]);
-    x[i] = fma(x[i], sg, p);
+    for (int i = 0; i < E; ++i) {
+      const int u = __float_as_int(x[i]);
+      const auto r = m == 16 ? __builtin_amdgcn_permlane16_swap(u, u, false, false)
+                             : __builtin_amdgcn_permlane32_swap(u, u, false, false);
+      x[i] = fma(__int_as_float((int)r[1]), sg, __int_as_float((int)r[0]));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const real p = xor_lane<m>(x[i]);
+      x[i] = fma(x[i], sg, p);
+    }
   }
 }
 
@@ -208,7 +224,10 @@ template <typename real> __device__ __forceinline__ real dsqrt(real x);
 template <> __device__ __forceinline__ float dsqrt<float>(float x) { return sqrtf(x); }
 template <> __device__ __forceinline__ double dsqrt<double>(double x) { return sqrt(x); }
 template <typename real> __device__ __forceinline__ real dexp(real x);
-template <> __device__ __forceinline__ float dexp<float>(float x) { return expf(x); }
+// binary32: the native v_exp_f32 (exp2 of x log2 e; relative error ~1e-7 near
+// the section maximum, ~5e-6 at e^-87), well inside the fp32 parity bound,
+// instead of the ~10-instruction range-reduced expf
+template <> __device__ __forceinline__ float dexp<float>(float x) { return __expf(x); }
 template <> __device__ __forceinline__ double dexp<double>(double x) { return exp(x); }
 template <typename real> __device__ __forceinline__ real neg_inf();
 template <> __device__ __forceinline__ float neg_inf<float>() { return -INFINITY; }

@@ -13,17 +13,19 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
      python3 bench.py --no-cpu --no-dense "$@" > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
 python3 - "$OUT" <<'PY'
-import csv, glob, sys, collections
+import csv, glob, sys, collections, os
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(sys.argv[1])), "..", "scripts"))
+sys.path.insert(0, "scripts")
+from pmc_summary import short
 out = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].split("::")[-1][:40]
-        acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, d in acc.items():
+        acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, d in sorted(acc.items()):
     if not (k.startswith("k_sec") or k.startswith("k_row")):
         continue
-    print(k)
+    print(k, "(per launch, mean over launches; SQ_* cycle counters in quad-cycles)")
     for c, v in sorted(d.items()):
         print(f"   {c:28s} {sum(v)/len(v):16.1f}")
 PY

@@ -289,3 +289,62 @@ def test_full_size_properties_c4(sp):
     assert np.array_equal(orc.section_argmax(b, L, M), idx)
     # β̂ is a per-section posterior scaled by sqrt(n Pl): rows sum to that
     assert np.allclose(b.reshape(L, M).sum(1), np.sqrt(n * Pl), rtol=1e-4)
+
+
+@pytest.mark.parametrize("B", [1, 6])
+def test_profile_rep_and_plan(sp, B):
+    """sa_profile / sa_profile_rep (the bench's roofline timing): positive
+    per-kernel means, one section + one row launch per iteration, and a
+    subsequent run still decodes correctly (rep mode leaves garbage behind)."""
+    L, M, T = 64, 512, 6
+    n = int(L * np.log2(M))
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n))
+    Pl = 2.0 / L * np.ones(L)
+    Ab, Az, _ = orc.sparc_transforms(L, M, n)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.5, Ab, 70 + i)[1].reshape(-1) for i in range(B)])
+    op.reserve(B, T)
+    op.stage(ys, Pl)
+    plan = op.plan(B)
+    assert plan["section_kernel"] in op.SECTION_KERNELS and plan["partials"] > 0
+    kinds, total = op.profile(B, T, early_stop=False)
+    assert kinds["k_sec"][1] == T and kinds["k_row"][1] == T + 1 and total > 0
+    kinds_rep, _ = op.profile(B, 2, early_stop=False, rep=8)
+    assert kinds_rep["k_sec"][0] > 0 and kinds_rep["k_sec"][1] == 2
+    with pytest.raises(AssertionError):  # SA_ERR_ARG: the reference's AssertionError cases
+        op.profile(B, T, rep=0)
+    bb, _ = op.amp_batch(ys, Pl, T, early_stop=False)
+    for i in range(B):
+        ref, _ = orc.amp_test(ys[i], 0, Pl, L, M, T, Ab, Az)
+        assert rel(bb[i], ref) <= TOL["fp32"]
+
+
+def test_power_batch_errors(sp):
+    """sa_stage_power_batch: shape, sign and backend checks; a later shared
+    allocation returns to it (graphs keyed on the mode)."""
+    L, M, T = 16, 8, 8
+    n = int(L * np.log2(M))
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp64")
+    Pl = 2.0 / L * np.ones(L)
+    Ab, Az, _ = orc.sparc_transforms(L, M, n)
+    _, y = orc.rep_inputs(L, M, n, Pl, 0.4, Ab, 3)
+    op.reserve(1, T)
+    op.stage(y.reshape(1, -1), Pl)
+    with pytest.raises(AssertionError):
+        op.stage_power_batch(1, Pl)  # must be (B, L)
+    bad = Pl.copy()[None, :]
+    bad[0, 3] = -1.0
+    with pytest.raises(AssertionError):
+        op.stage_power_batch(1, bad)
+    op.stage_power_batch(1, Pl[None, :])
+    op.run(1, T)
+    op.wait()
+    b_pb, _ = op.fetch(1)
+    op.stage_power(1, Pl)
+    op.run(1, T)
+    op.wait()
+    b_sh, _ = op.fetch(1)
+    assert np.array_equal(b_pb, b_sh)
+    dense = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="dense")
+    dense.reserve(1, T)
+    with pytest.raises(sp.SparcAmpError):  # SA_ERR_UNSUPPORTED
+        dense.stage_power_batch(1, Pl[None, :])

@@ -19,7 +19,7 @@ from .joint import (JointDecoder, joint_decoder, soft_amp_ldpc_sim, hardinitbeta
                     waterfall, sp2bp, bp2sp, mc_joint)
 from . import threshold
 from .threshold import (hard_initialisation, prep_y, calc_E, hist_E, calc_I_e, J, J_inverse,
-                        soft_amp_ldpc_hardinit, ber_from_LLRs, soft_hardinit_plot)
+                        soft_amp_ldpc_hardinit, ber_from_LLRs, soft_hardinit_plot, calc_E_batch, amp_exit_curve)
 from . import dist
 
 __version__ = "0.1.0"

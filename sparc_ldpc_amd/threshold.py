@@ -13,6 +13,7 @@ sp2bp + LLRs (``sa_llr``), and BP.  AMP runs in fp64 (see joint.joint_decoder).
 from __future__ import annotations
 
 import csv
+import sys
 import math
 
 import numpy as np
@@ -22,7 +23,8 @@ from .harness import SPARCParams, LDPCParams, pa_parameterised, _popcount
 from .operators import AbOp, SparcOperator, make_ordering, sparc_transforms_shorter
 
 __all__ = ["J", "J_inverse", "gen_bits", "hard_initialisation", "prep_y", "remove_common_zeros", "calc_E",
-           "hist_E", "calc_I_e", "polynomial", "soft_amp_ldpc_hardinit", "ber_from_LLRs", "soft_hardinit_plot"]
+           "hist_E", "calc_I_e", "polynomial", "soft_amp_ldpc_hardinit", "ber_from_LLRs", "soft_hardinit_plot",
+           "exit_draws", "calc_E_batch", "amp_exit_curve"]
 
 _RLDPC = {"5/6": 5 / 6, "1/2": 1 / 2, "0.45": 0.45, "3/8": 3 / 8}  # sparc_ldpc.py:1458-1467
 
@@ -360,3 +362,105 @@ def soft_hardinit_plot(sparcparams: SPARCParams, ldpcparams: LDPCParams, csv_fil
                 wr.writerow({"EbN0_dB": r["EbN0_dB"], "BER_amp": np.array(r["BER_amp"]),
                              "BER_ldpc": np.array(r["BER_ldpc"]), "BER_plain": r["BER_plain"]})
     return rows
+
+
+# ---- batched EXIT measurement (amp_exit.py:185-270, 520-631) ------------------------
+
+_MASKED = {}
+
+
+def exit_draws(items, L, M, n, P, rng=np.random):
+    """The np.random draws of a sequence of calc_E calls as amp_exit_curve makes
+    them (amp_exit.py:581-589, 218-219, 153): per item (I_a, snr_dB) in order,
+    X = gen_bits(L log2 M), N_a = randn(L log2 M) sigma_a, w = randn(n, 1) sigma_w.
+    Returns X (B, L logm) +-1, A = mu_a X + N_a (B, L logm), w (B, n)."""
+    logm = int(round(math.log2(M)))
+    B = len(items)
+    X = np.empty((B, L * logm), dtype=np.int64)
+    A = np.empty((B, L * logm))
+    w = np.empty((B, n))
+    for b, (I_a, snr_dB) in enumerate(items):
+        X[b] = (rng.randint(0, 2, L * logm) * -2) + 1                     # gen_bits, :48-50
+        sigma_a = J_inverse(I_a)
+        A[b] = (sigma_a ** 2) / 2 * X[b] + rng.randn(L * logm) * sigma_a  # :215-222
+        sigma_w = np.sqrt(P / 10 ** (snr_dB / 20))                        # :205-206
+        w[b] = rng.randn(n, 1).reshape(-1) * sigma_w                      # prep_y, :153
+    return X, A, w
+
+
+def calc_E_batch(X, A, w, sparcparams: SPARCParams, threshold=0.5, precision="fp64"):
+    """calc_E (amp_exit.py:185-270) for B calls at once: every section whose
+    a-priori bp2sp has exactly one entry above the threshold is decided and
+    cancelled from y; AMP then runs over each codeword's own undecided
+    sections (a per-codeword section mask, SparcOperator.stage_power_batch,
+    instead of one shortened operator per call) and their LLRs replace A;
+    clipped to +-55.  X, A: (B, L log2 M); w: (B, n).  Returns E (B, L log2 M)."""
+    L, M, P, T = sparcparams.L, sparcparams.M, sparcparams.p, sparcparams.t
+    logm = int(np.log2(M))
+    n = int(L * np.log2(M) / sparcparams.r)
+    X = np.asarray(X)
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    B = X.shape[0]
+    a, f, C = sparcparams.a, sparcparams.f, sparcparams.C
+    Pl = P / L * np.ones(L) if a is None else pa_parameterised(L, C, P, a, f)
+    Xb = ((X - 1) * -1 // 2).astype(np.int64).reshape(B, L, logm)
+    idx = (Xb * (1 << np.arange(logm - 1, -1, -1))).sum(axis=2).astype(np.int32)
+    op = _op(L, M, n, 0, precision)
+    op.reserve(B, T)
+    op.stage_power(B, Pl)
+    op.encode(idx, np.ascontiguousarray(w, dtype=np.float64).reshape(B, n))
+    dec = op.threshold(B, 0, L, A, threshold)  # every section is thresholded
+    E = A.copy()
+    und = dec < 0
+    if und.any():
+        key = (L, M, n, precision)
+        mk = _MASKED.get(key)
+        if mk is None:
+            mk = _MASKED[key] = op.subset(np.arange(L))
+        mk.reserve(B, T)
+        mk.stage_power(B, Pl)  # c_l of the LLR kernel
+        op.cancel(dec, mk)
+        mk.stage_power_batch(B, np.where(und, Pl[None, :], 0.0))
+        mk.run(B, T)
+        mk.wait()
+        llr = mk.llr(B, 0, L).reshape(B, L, logm)
+        E.reshape(B, L, logm)[und] = llr[und]
+    np.clip(E, -55, 55, out=E)
+    return E
+
+
+def amp_exit_curve(sparcparams: SPARCParams, low_snr_dB, high_snr_dB, repeats, x_axis_points, threshold,
+                   poly_curve=0, bin_number=500, batch=256, precision="fp64", export_csv_filename=None):
+    """amp_exit_curve (amp_exit.py:520-631) on the GPU: the AMP EXIT curves of
+    threshold-initialised exchange at 4 SNRs (linspace(low, high, 4) dB,
+    20 log10), I_a = linspace(0, 0.99, x_axis_points), averaged over
+    `repeats`; histograms with bin_number bins over [-60, 60]; the cubic fit
+    of curve `poly_curve`.  The calc_E calls draw from the global np.random
+    stream in the reference's order (repeat, SNR, I_a) and are decoded
+    `batch` at a time (calc_E_batch).  No plots and no CSV import (analysis
+    and figure code are out of scope); export_csv_filename appends the
+    reference's rows (I_a, snr_dB, X, E), arrays written in full.
+    Returns (I_a_range, snr_dB, I_e (4, x_axis_points), poly_coeff)."""
+    L, M, P = sparcparams.L, sparcparams.M, sparcparams.p
+    n = int(L * np.log2(M) / sparcparams.r)
+    curves = 4
+    I_a_range = np.linspace(0, 0.99, x_axis_points)
+    snr_dB = np.linspace(low_snr_dB, high_snr_dB, curves)
+    items = [(k, j, i) for k in range(repeats) for j in range(curves) for i in range(x_axis_points)]
+    I_e_accum = np.zeros((curves, x_axis_points))
+    for s0 in range(0, len(items), batch):
+        chunk = items[s0:s0 + batch]
+        X, A, w = exit_draws([(I_a_range[i], snr_dB[j]) for (_, j, i) in chunk], L, M, n, P)
+        E = calc_E_batch(X, A, w, sparcparams, threshold, precision)
+        for b, (_, j, i) in enumerate(chunk):
+            if export_csv_filename is not None:
+                with open(export_csv_filename, "a") as fh:
+                    wr = csv.DictWriter(fh, fieldnames=["I_a", "snr_dB", "X", "E"])
+                    wr.writeheader()
+                    full = dict(threshold=sys.maxsize, max_line_width=sys.maxsize)
+                    wr.writerow({"I_a": I_a_range[i], "snr_dB": snr_dB[j], "X": np.array2string(X[b], **full),
+                                 "E": np.array2string(E[b], **full)})
+            PE_pos, PE_neg, _, _, _, _, bw = hist_E(X[b], E[b], bin_number=bin_number, max_bin=60, min_bin=-60)
+            I_e_accum[j, i] += calc_I_e(PE_pos, PE_neg, bw)
+    I_e_accum /= repeats
+    return I_a_range, snr_dB, I_e_accum, polynomial(I_a_range, I_e_accum[poly_curve, :])

@@ -158,3 +158,57 @@ def test_power_batch_mask_equals_shortened_operator(L, M, n, B):
         sAb, sAz = orc.sparc_transforms_shorter(len(keep), M, n, oord[keep])
         refb = orc.amp(yb, 0, Pl[keep], len(keep), M, T, sAb, sAz).reshape(len(keep), M)
         np.testing.assert_allclose(got[b].reshape(L, M)[keep], refb, rtol=0, atol=1e-9 * np.abs(refb).max())
+
+
+def test_calc_E_batch_matches_reference():
+    """The reference's calc_E reps (tests/golden/joint.npz) decoded as one batch
+    (calc_E_batch: per-codeword section masks), draws replayed by exit_draws."""
+    import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd import threshold as th
+    g = golden("joint.npz")
+    L, M, P, r, T = g["exit|cfg"]
+    L, M, T = int(L), int(M), int(T)
+    spp = sp.SPARCParams(L, M, None, float(P), float(r), T)
+    n = int(L * np.log2(M) / float(r))
+    keys = _keys("exit|")
+    Xs, As, ws, thrs = [], [], [], []
+    for key in keys:
+        I_a, snr_db, thr = g[key + "|par"]
+        s = int(key.split("|")[1])
+        X, A, w = th.exit_draws([(float(I_a), float(snr_db))], L, M, n, float(P), np.random.RandomState(100 + s))
+        assert np.array_equal(X[0], g[key + "|X"])
+        Xs.append(X[0]); As.append(A[0]); ws.append(w[0]); thrs.append(float(thr))
+    E = np.empty((len(keys), len(Xs[0])))
+    for thr in set(thrs):  # one batch per threshold
+        sel = [b for b in range(len(keys)) if thrs[b] == thr]
+        E[sel] = th.calc_E_batch(np.stack([Xs[b] for b in sel]), np.stack([As[b] for b in sel]),
+                                 np.stack([ws[b] for b in sel]), spp, thr)
+    for b, key in enumerate(keys):
+        Er = g[key + "|E"]
+        mid = np.abs(Er) < 50
+        np.testing.assert_allclose(E[b][mid], Er[mid], rtol=1e-8, atol=1e-8)
+        assert np.array_equal(np.sign(E[b][~mid]), np.sign(Er[~mid]))
+
+
+def test_amp_exit_curve_matches_sequential_calc_E():
+    """amp_exit_curve (amp_exit.py:520-631), batched, against the same sweep
+    made of per-codeword calc_E calls in the reference's draw order."""
+    import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd import threshold as th
+    spp = sp.SPARCParams(64, 16, None, 4.0, 1.0, 30)
+    reps, pts, thr = 2, 4, 0.7
+    np.random.seed(123)
+    I_a, snr, I_e, poly = th.amp_exit_curve(spp, 6.0, 12.0, reps, pts, thr, bin_number=125, batch=11)
+    assert I_e.shape == (4, pts) and np.all((I_e >= 0) & (I_e <= 1)) and poly.shape == (4,)
+    np.random.seed(123)
+    ref = np.zeros((4, pts))
+    for k in range(reps):
+        for j, s in enumerate(snr):
+            for i, ia in enumerate(I_a):
+                X = th.gen_bits(64 * 4)
+                E = th.calc_E(X, ia, s, spp, None, thr)
+                h = th.hist_E(X, E, bin_number=125, max_bin=60, min_bin=-60)
+                ref[j, i] += th.calc_I_e(h[0], h[1], h[6])
+    ref /= reps
+    np.testing.assert_allclose(I_e, ref, rtol=0, atol=1e-6)
+    assert I_e[:, -1].mean() > I_e[:, 0].mean()  # more a-priori information, more extrinsic

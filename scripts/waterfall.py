@@ -13,6 +13,10 @@
             initialised exchange, L=M=512 P=4 r_sparc=1 T=64 + 802.16 rate 5/6
             over all 512 sections, soft_iter=2, sigma = linspace(0.9, 1.4, 10),
             threshold 0.6 or 0.8 (--threshold), MIN_ERRORS = MAX_BLOCKS = 200.
+  soft_hard : soft_hard_plot() (sparc_ldpc.py:1285-1432) in full: L=768 M=512
+            P=1.8 r_sparc=1 T=64, 802.16 5/6 with sec=569 (z=213), soft
+            exchange (2 rounds) and the original hard exchange,
+            sigma = linspace(0.8, 0.4, 10), MIN_ERRORS = MAX_BLOCKS = 100.
   l768    : soft_hard_plot()'s BER_sparc column (sparc_ldpc.py:1285-1432):
             L=768 M=512 P=1.8 at the overall rate R=0.8765 (sec=569),
             sigma = linspace(0.8, 0.4, 10), 100 reps per point.
@@ -34,7 +38,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sweep", default="plain", choices=["plain", "l768", "soft", "hard", "originalHard", "threshold"])
+    ap.add_argument("--sweep", default="plain", choices=["plain", "l768", "soft", "hard", "originalHard", "threshold", "soft_hard"])
     ap.add_argument("--threshold", type=float, default=0.6)
     ap.add_argument("--reps", type=int, default=0,
                     help="l768: reps per sigma point (default: the published 100; BASELINE configs[3] is 1000 x 10)")
@@ -75,6 +79,20 @@ def main():
         ref = pub["waterfall_joint"]["runs"][args.sweep]
         for i, r in enumerate(rows):
             r["reference"] = {k: ref[k][i] for k in ref if k not in ("file", "EbN0_dB")}
+    elif args.sweep == "soft_hard":
+        cfg = pub["soft_hard"]["config"]
+        spp = sp.SPARCParams(cfg["L"], cfg["M"], None, cfg["P"], cfg["r_sparc"], cfg["T"])
+        lp = sp.LDPCParams(cfg["standard"], cfg["r_ldpc"], None)
+        sig = np.linspace(*cfg["sigma"])[:args.points]
+        rows = sp.soft_hard_plot(True, True, cfg["sec"], cfg["soft_iter"], spp, lp,
+                                 args.out + ".csv" if rank == 0 else None, None, MIN_ERRORS=cfg["MIN_ERRORS"],
+                                 MAX_BLOCKS=cfg["MAX_BLOCKS"], batch=args.batch, precision=args.precision,
+                                 rank=rank, world=world, allreduce=dist.allreduce_sum, sigmas=sig)
+        ps, ph = pub["soft_hard"]["soft"], pub["soft_hard"]["hard"]
+        for i, r in enumerate(rows):
+            r["reference"] = dict(BER_sparc=ps["BER_sparc"][i], BER_ldpc_soft=ps["BER_ldpc"][i],
+                                  BER_amp_soft=ps["BER_amp"][i], BER_ldpc_hard=ph["BER_ldpc"][i],
+                                  BER_amp_hard=ph["BER_amp"][i])
     elif args.sweep == "threshold":
         cfg = pub["threshold_init"]["config"]
         spp = sp.SPARCParams(cfg["L"], cfg["M"], None, cfg["P"], cfg["r_sparc"], cfg["T"])

@@ -15,7 +15,7 @@ from .harness import (SPARCParams, LDPCParams, pa_parameterised, bits2indices, b
                       amp_test_reps)
 from . import ldpc
 from .ldpc import code, LdpcBpError
-from .joint import (JointDecoder, joint_decoder, soft_amp_ldpc_sim, hardinitbeta_amp_ldpc_sim, sim_ldpc,
+from .joint import (JointDecoder, joint_decoder, soft_amp_ldpc_sim, hardinitbeta_amp_ldpc_sim, sim_ldpc, soft_hard_plot,
                     waterfall, sp2bp, bp2sp, mc_joint)
 from . import threshold
 from .threshold import (hard_initialisation, prep_y, calc_E, hist_E, calc_I_e, J, J_inverse,

@@ -39,7 +39,7 @@ from .harness import SPARCParams, LDPCParams, pa_parameterised, ebno_to_sigma
 from .operators import SparcOperator, make_ordering
 
 __all__ = ["JointDecoder", "joint_decoder", "draw_reps", "amp_ldpc_sim_ldpc", "soft_amp_ldpc_sim",
-           "hardinitbeta_amp_ldpc_sim", "sim_ldpc", "waterfall", "sp2bp", "bp2sp", "mc_joint"]
+           "hardinitbeta_amp_ldpc_sim", "sim_ldpc", "waterfall", "soft_hard_plot", "sp2bp", "bp2sp", "mc_joint"]
 
 MODES = ("originalHard", "soft", "hard", "threshold")
 
@@ -493,3 +493,82 @@ def _ber_point_multi(round_fn, total_bits, min_errors, max_blocks, batch, rank, 
             break
         rnd += 1
     return dict(BER=ber_cum / nblocks, cols=(cum / nblocks).tolist(), blocks=nblocks, block_errors=nerr)
+
+
+# ---- soft_hard_plot (sparc_ldpc.py:1285-1432) ----------------------------------------------
+
+def soft_hard_plot(soft, hard, sec, soft_iter, sparcparams: SPARCParams, ldpcparams: LDPCParams, csv_filename=None,
+                   png_filename=None, datapoints=10, MIN_ERRORS=100, MAX_BLOCKS=500, batch=64, seed0=0,
+                   backend=None, precision=None, rank=0, world=1, allreduce=None, sigmas=None):
+    """Soft exchange vs the original hard exchange on the GPU.
+
+    The LDPC code covers nl = log2(M) * sec bits with z = int(nl / 24)
+    (802.16 rate 5/6: N = 24 z bits, i.e. N / log2 M sections); overall rate
+    R = (L log2 M - nl / 6) / n (:1309-1314, the 5/6 hard-coded as there).
+    Per sigma of linspace(0.8, 0.4, datapoints) (:1322): BER_sparc = mean over
+    MIN_ERRORS plain-SPARC reps at rate R (:1334-1337); soft: soft_amp_ldpc_sim
+    blocks until MIN_ERRORS blocks with LDPC errors after round 1 or
+    MAX_BLOCKS (:1339-1353); hard: amp_ldpc_sim (LDPC branch) blocks with the
+    same rule (:1354-1369).  Blocks are seeded and batched (mc_joint) and
+    sharded over ranks like waterfall.  Returns rows (EbN0_dB, BER_sparc,
+    BER_ldpc_soft [soft_iter], BER_amp_soft [soft_iter + 1], BER_ldpc_hard,
+    BER_amp_hard [2], blocks); rank 0 appends the reference's two CSV blocks
+    (:1397-1413).  No plots."""
+    from .harness import mc_decode
+    from .dist import shard_seeds
+    precision = precision or "fp64"
+    L, M, p, r_sparc, T = sparcparams.L, sparcparams.M, sparcparams.p, sparcparams.r, sparcparams.t
+    logm = int(np.log2(M))
+    nl = logm * sec
+    z = int(nl / 24)
+    ldp = LDPCParams(ldpcparams.standard, ldpcparams.r_ldpc, z, ldpcparams.ptype)
+    n_f = L * logm / r_sparc
+    R = (L * logm - nl * (1 - 5 / 6)) / n_f
+    n = int(L * np.log2(M) / r_sparc)
+    n_plain = int(L * np.log2(M) / R)
+    total_bits = L * logm
+    Pl = p / L * np.ones(L)
+    jd = joint_decoder(L, M, n, ldp, T, backend=backend, precision=precision)
+    plain = SparcOperator(L, M, n_plain, make_ordering(L, M, n_plain, 0), backend, precision)
+    SIGMA = np.linspace(0.8, 0.4, datapoints) if sigmas is None else np.asarray(sigmas, dtype=np.float64)
+    rows = []
+    for pi, sigma in enumerate(SIGMA):
+        sigma = float(sigma)
+        base = seed0 + pi * 10_000_000
+        seeds = [s for s in range(base + 5_000_000, base + 5_000_000 + MIN_ERRORS) if s % world == rank]
+        be_plain, _ = mc_decode(plain, Pl, sigma, T, seeds, batch=batch)
+        tot = np.array([int(be_plain.sum())], dtype=np.int64)
+        if allreduce is not None:
+            tot = allreduce(tot)
+        row = dict(EbN0_dB=float(20 * np.log10(1 / (2 * R) * (p / sigma ** 2))), sigma=sigma,
+                   BER_sparc=float(tot[0]) / (MIN_ERRORS * total_bits))
+        for mode, on in (("soft", soft), ("originalHard", hard)):
+            if not on:
+                continue
+
+            def round_fn(sds, mode=mode, sigma=sigma):
+                rj = mc_joint(jd, Pl, sigma, sds, mode, soft_iter, batch)
+                if mode == "soft":
+                    return rj["ldpc"][:, 0], np.concatenate([rj["ldpc"], rj["amp"]], axis=1)
+                cols = [rj["ldpc"][:, 0], rj["amp"][:, 0], rj.get("ldpc_amp", 0 * rj["amp"][:, 0])]
+                return rj["ldpc"][:, 0], np.stack(cols, axis=1)
+
+            res = _ber_point_multi(round_fn, total_bits, MIN_ERRORS, MAX_BLOCKS, batch, rank, world, allreduce,
+                                   base + (0 if mode == "soft" else 2_500_000))
+            c = res["cols"]
+            if mode == "soft":
+                row.update(BER_ldpc_soft=c[:soft_iter], BER_amp_soft=c[soft_iter:], blocks_soft=res["blocks"])
+            else:
+                row.update(BER_ldpc_hard=c[0], BER_amp_hard=[c[1], c[2]], blocks_hard=res["blocks"])
+        rows.append(row)
+    if csv_filename and rank == 0:
+        for mode, fields in (("soft", ["EbN0_dB", "BER_sparc", "BER_ldpc_soft", "BER_amp_soft"]),
+                             ("hard", ["EbN0_dB", "BER_sparc", "BER_ldpc_hard", "BER_amp_hard"])):
+            if not (soft if mode == "soft" else hard):
+                continue
+            with open(csv_filename, "a", newline="") as fh:
+                wr = csv.DictWriter(fh, fieldnames=fields)
+                wr.writeheader()
+                for row in rows:
+                    wr.writerow({k: (np.array(row[k]) if isinstance(row[k], list) else row[k]) for k in fields})
+    return rows

@@ -1,7 +1,7 @@
-"""Adds the published threshold-initialised exchange curves to
-published_ber.json (numbers copied as data from the reference's CSVs; build
-container only, needs /root/reference).
+"""Adds published BER curves to published_ber.json (numbers copied as data
+from the reference's CSVs; build container only, needs /root/reference).
 
+threshold_init:
 soft_hardinit_plot (sparc_ldpc.py:1435-1590) with L=M=512 P=4 r_sparc=1 T=64,
 802.16 rate 5/6 over all 512 sections, soft_iter=2, sigma = linspace(0.9, 1.4, 10):
   thresholdinit_LM512Rsparc1P4_stndrd80216_Rldpc5_6_it2_rep200_threshold0_6.csv (two runs)
@@ -49,9 +49,45 @@ def parse(path):
     return runs
 
 
+def parse_soft_hard(path):
+    """EbN0VsBER_soft_hard_100_4.csv: a soft block (EbN0_dB, BER_sparc,
+    BER_ldpc_soft [2], BER_amp_soft [3]) then a hard block (EbN0_dB, BER_sparc,
+    BER_ldpc_hard, BER_amp_hard [2])."""
+    out, cur = {}, None
+    for line in open(path):
+        line = line.strip()
+        if not line:
+            continue
+        if line.startswith("EbN0_dB"):
+            cur = "soft" if "soft" in line else "hard"
+            out[cur] = dict(EbN0_dB=[], BER_sparc=[], BER_ldpc=[], BER_amp=[])
+            continue
+        head, sp_, rest = line.split(",", 2)
+        d = out[cur]
+        d["EbN0_dB"].append(float(head))
+        d["BER_sparc"].append(float(sp_))
+        if cur == "soft":
+            e = rest.index("]")
+            d["BER_ldpc"].append(vec(rest[:e + 1]))
+            d["BER_amp"].append(vec(rest[e + 2:]))
+        else:
+            ldpc, amp = rest.split(",", 1)
+            d["BER_ldpc"].append(float(ldpc))
+            d["BER_amp"].append(vec(amp))
+    return out
+
+
 def main():
     p = os.path.join(HERE, "published_ber.json")
     pub = json.load(open(p))
+    # soft_hard_plot (sparc_ldpc.py:1285-1432, __main__ :1672-1674): L=768 M=512
+    # P=1.8 r_sparc=1 T=64, 802.16 5/6 with sec=569 (z=213), soft_iter=2,
+    # sigma = linspace(0.8, 0.4, 10), MIN_ERRORS = MAX_BLOCKS = 100
+    pub["soft_hard"] = dict(
+        config=dict(L=768, M=512, P=1.8, r_sparc=1, T=64, standard="802.16", r_ldpc="5/6", sec=569, soft_iter=2,
+                    sigma=[0.8, 0.4, 10], MIN_ERRORS=100, MAX_BLOCKS=100,
+                    file="EbN0VsBER_soft_hard_100_4.csv"),
+        **parse_soft_hard(os.path.join(REF, "EbN0VsBER_soft_hard_100_4.csv")))
     runs = []
     for f, thr in FILES.items():
         for r in parse(os.path.join(REF, f)):

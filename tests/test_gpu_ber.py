@@ -82,3 +82,31 @@ def test_threshold_init_overlays_reference(lib_gpu, unit_cancel):
                 continue
             ref = [(x["BER_amp"][i] + x["BER_ldpc"][i] + [x["BER_plain"][i]])[j] for x in refs]
             assert min(ref) / 1.5 <= v <= max(ref) * 1.5, (r["EbN0_dB"], j, v, ref)
+
+
+def test_soft_hard_plot_overlays_reference(lib_gpu):
+    """soft_hard_plot (sparc_ldpc.py:1285-1432) at L=768 with the 802.16 5/6
+    code over 568 sections (sec=569, z=213): at the points whose columns are
+    all >= 1e-3 (sigma 0.8 and 0.756: 4.1 and 5.1 dB) every column falls within
+    1.5x of the reference's single published run."""
+    import sparc_ldpc_amd as sp
+    with open(os.path.join(GOLDEN, "published_ber.json")) as fh:
+        pub = json.load(fh)["soft_hard"]
+    c = pub["config"]
+    pts = [0, 1]
+    sig = np.linspace(*c["sigma"])[pts]
+    spp = sp.SPARCParams(c["L"], c["M"], None, c["P"], c["r_sparc"], c["T"])
+    rows = sp.soft_hard_plot(True, True, c["sec"], c["soft_iter"], spp, sp.LDPCParams(c["standard"], c["r_ldpc"], None),
+                             MIN_ERRORS=c["MIN_ERRORS"], MAX_BLOCKS=c["MAX_BLOCKS"], batch=64, sigmas=sig)
+    ps, ph = pub["soft"], pub["hard"]
+
+    def near(v, ref):
+        return ref / 1.5 <= v <= ref * 1.5
+
+    for i, r in zip(pts, rows):
+        assert abs(r["EbN0_dB"] - ps["EbN0_dB"][i]) < 1e-9
+        assert near(r["BER_sparc"], ps["BER_sparc"][i]), (r["EbN0_dB"], r["BER_sparc"], ps["BER_sparc"][i])
+        for v, ref in zip(r["BER_ldpc_soft"] + r["BER_amp_soft"], ps["BER_ldpc"][i] + ps["BER_amp"][i]):
+            assert near(v, ref), (r["EbN0_dB"], "soft", v, ref)
+        for v, ref in zip([r["BER_ldpc_hard"]] + r["BER_amp_hard"], [ph["BER_ldpc"][i]] + ph["BER_amp"][i]):
+            assert near(v, ref), (r["EbN0_dB"], "hard", v, ref)

@@ -24,7 +24,7 @@ from .operators import SparcOperator, make_ordering, sparc_transforms, sparc_tra
 
 __all__ = [
     "SPARCParams", "LDPCParams", "pa_parameterised", "bits2indices", "ber_of",
-    "amp_ldpc_sim", "mc_decode", "ebno_to_sigma", "ber_point", "waterfall_plain", "amp_test_reps",
+    "amp_ldpc_sim", "mc_decode", "ebno_to_sigma", "ber_point", "waterfall_plain", "amp_test_reps", "amp_init_test",
 ]
 
 
@@ -279,3 +279,27 @@ def amp_test_reps(L=512, M=512, L_zero=154, P=4, snr_dB=10, r_sparc=1, T=64, rep
         bz = amp(y, sigma, Pl, L, M, T, Ab, Az).reshape(-1)
         ber_no_init += ber_of(idx, bz.reshape(L, M).argmax(1), total_bits)
     return ber_hard / repeats, ber_soft / repeats, ber_no_init / repeats
+
+
+def amp_init_test(L, M, snr_dB, P, r_sparc, backend=None, precision=None):
+    """amp_test.py:53-110: one rep decoded twice, from the transmitted beta
+    itself and from zero (amp_test with T = 64); returns ([ber_init],
+    [ber_no_init]) and prints the iteration counts like the reference.
+    Draws: np.random randint(0, 2, L log2 M) then randn(n, 1) sigma."""
+    logm = np.log2(M)
+    total_bits = int(L * logm)
+    sigma = np.sqrt(P / 10 ** (snr_dB / 20))
+    n = int(L * np.log2(M) / r_sparc)
+    Pl = P / L * np.ones(L)
+    idx = np.asarray(bits2indices(np.random.randint(0, 2, total_bits).tolist(), M))
+    Ab, Az, _ = sparc_transforms(L, M, n, backend=backend, precision=precision)
+    beta = np.zeros((L * M, 1))
+    beta[np.arange(L) * M + idx, 0] = np.sqrt(n * Pl)
+    y = (Ab(beta) + np.random.randn(n, 1) * sigma).reshape(-1, 1)
+    beta_init, t_init = amp_test(y, 0, Pl, L, M, 64, Ab, Az, beta)
+    beta_no_init, t_no_init = amp_test(y, 0, Pl, L, M, 64, Ab, Az)
+    ber_init = [float(ber_of(idx, beta_init.reshape(L, M).argmax(1), total_bits))]
+    ber_no_init = [float(ber_of(idx, beta_no_init.reshape(L, M).argmax(1), total_bits))]
+    print("For initialised amp, BER= ", ber_init, " and iterations= ", t_init)
+    print("For amp with all zero beta_0, BER= ", ber_no_init, " and iterations= ", t_no_init)
+    return ber_init, ber_no_init

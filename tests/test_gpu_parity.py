@@ -348,3 +348,13 @@ def test_power_batch_errors(sp):
     dense.reserve(1, T)
     with pytest.raises(sp.SparcAmpError):  # SA_ERR_UNSUPPORTED
         dense.stage_power_batch(1, Pl[None, :])
+
+
+def test_amp_init_test(sp, capsys):
+    """amp_test.py:53-110: started from the transmitted beta, AMP keeps every
+    section and stops almost at once; the zero start at high SNR also decodes."""
+    np.random.seed(4)
+    b_init, b_no = sp.amp_init_test(64, 64, 15.0, 4.0, 1.0)
+    assert b_init == [0.0] and b_no == [0.0]
+    out = capsys.readouterr().out
+    assert "For initialised amp, BER=  [0.0]" in out and "all zero beta_0" in out

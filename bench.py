@@ -158,11 +158,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # SPARC_BENCH_DIST=gloo: rehearsal of the N-rank path on a box with fewer
+    # GPUs than ranks (ranks share device LOCAL_RANK % device_count); the
+    # driver's multi-GPU runs use the default, RCCL with one GPU per rank
+    backend = os.environ.get("SPARC_BENCH_DIST", "nccl")
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL over xGMI
+        if backend != "nccl":
+            device = local % torch.cuda.device_count()
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend)  # "nccl" = RCCL over xGMI
 
     import sparc_ldpc_amd as sp
 
@@ -172,7 +179,6 @@ def main():
     L, M, P, T, B, sigma = w["L"], w["M"], w["P"], w["T"], w["B"], w["sigma"]
     n = n_of(w)
     Pl = P / L * np.ones(L)
-    device = local
     op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend=args.backend,
                           precision=args.precision, device=device)
     # per-rank synthetic reps: seeds 1000 + rank*B + i (sharded, no overlap)
@@ -198,7 +204,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

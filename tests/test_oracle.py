@@ -159,3 +159,24 @@ def test_bucket_factorisation_model(L, M, R):
         ab += sgr * t[o & (M - 1)]
     assert np.allclose(az / np.sqrt(n), Az(z).reshape(-1), rtol=0, atol=1e-12)
     assert np.allclose(ab / np.sqrt(n), Ab(b).reshape(-1), rtol=0, atol=1e-12)
+
+
+def test_c4_oracle_matches_reference():
+    """BASELINE configs[3] (L=768 M=512 R=5/6, w=16384): inputs, t=1 and the
+    converged decode at sigma=0.6 bit for bit (tests/golden/make_c4_golden.py)."""
+    g = golden("c4.npz")
+    L, M, n, T, NS = (int(g[k]) for k in ("L", "M", "n", "T", "NS"))
+    Ab, Az, ordering = orc.sparc_transforms(L, M, n)
+    assert sha(ordering) == str(g["ordering_sha256"])
+    Pl = float(g["P"]) / L * np.ones(L)
+    for k in (0, 1):
+        idx, y = orc.rep_inputs(L, M, n, Pl, float(g[f"sigma_{k}"]), Ab, 2000 + k)
+        assert np.array_equal(y, g[f"y_{k}"]) and np.array_equal(idx, g[f"idx_{k}"])
+        b1 = orc.amp(y, 0, Pl, L, M, 1, Ab, Az).astype(np.float32)
+        assert np.array_equal(b1[:NS * M], g[f"beta_t1_{k}"])
+        assert float(np.linalg.norm(b1.astype(np.float64))) == float(g[f"beta_t1_norm_{k}"])
+    b, t = orc.amp_test(g["y_1"], 0, Pl, L, M, T, Ab, Az)
+    assert t == int(g["t_stop_1"])
+    assert np.array_equal(b[:NS * M].astype(np.float32), g["beta_final_1"])
+    assert np.array_equal(orc.section_argmax(b, L, M), g["argmax_final_1"])
+    assert float(np.linalg.norm(b)) == float(g["beta_final_norm_1"])

@@ -324,6 +324,40 @@ def test_full_size_properties_c4(sp):
     assert np.allclose(b.reshape(L, M).sum(1), np.sqrt(n * Pl), rtol=1e-4)
 
 
+@pytest.mark.parametrize("prec,L,M,n", [("fp32", 6, 512, 38000),    # w = 65536, z fills the LDS
+                                         ("fp32", 3, 4096, 24000),   # M at its maximum, w = 32768
+                                         ("fp64", 5, 512, 18000)])   # w = 32768
+def test_maximum_sizes_vs_oracle(sp, prec, L, M, n):
+    """The largest n the section kernels stage in LDS (w up to 65536, the
+    uint16 table limit): operator, single-codeword and batched decodes
+    against the oracle; one step past the LDS limit is refused with an error,
+    never launched."""
+    Ab, Az, ordering = sp.sparc_transforms(L, M, n, precision=prec)
+    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
+    assert np.array_equal(ordering, oord)
+    rs = np.random.RandomState(n)
+    b = rs.randn(L * M, 1); z = rs.randn(n, 1)
+    assert rel(Ab(b), oAb(b)) <= TOL[prec]
+    assert rel(Az(z), oAz(z)) <= TOL[prec]
+    Pl = 3.0 / L * np.ones(L)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 40.0, oAb, 70 + i)[1].reshape(-1) for i in range(5)])
+    ref, t = orc.amp_test(ys[0], 0, Pl, L, M, 4, oAb, oAz)
+    assert t == 3
+    b1 = sp.amp(ys[0], 0, Pl, L, M, 4, Ab, Az)
+    assert rel(b1, ref) <= TOL[prec] and argmax_agree(b1, ref, L, M)
+    op = sp.SparcOperator(L, M, n, ordering, precision=prec)
+    if M <= 1024:  # the batched kernel's range
+        bb, _ = op.amp_batch(ys, Pl, 4, early_stop=False)
+        assert rel(bb[0], ref) <= TOL[prec]
+        ref4, _ = orc.amp_test(ys[4], 0, Pl, L, M, 4, oAb, oAz)
+        assert rel(bb[4], ref4) <= TOL[prec]
+    too_big = {"fp32": 40000, "fp64": 19000}[prec] if M == 512 else 25000
+    with pytest.raises(sp.SparcAmpError):
+        sp.SparcOperator(L, M, too_big, sp.make_ordering(L, M, too_big), precision=prec)
+    with pytest.raises(sp.SparcAmpError):
+        sp.SparcOperator(2, 8, 65535, sp.make_ordering(2, 8, 65535), precision=prec)
+
+
 @pytest.mark.parametrize("B", [1, 6])
 def test_profile_rep_and_plan(sp, B):
     """sa_profile / sa_profile_rep (the bench's roofline timing): positive

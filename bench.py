@@ -174,8 +174,9 @@ def main():
     import sparc_ldpc_amd as sp
 
     w = dict(WORKLOADS[args.workload])
-    if args.batch:
+    if args.batch and args.batch != w["B"]:
         w["B"] = args.batch
+        w["desc"] = w["desc"].split(", T=")[0] + f", T={w['T']}, batch of {args.batch} codeword(s) (--batch)"
     L, M, P, T, B, sigma = w["L"], w["M"], w["P"], w["T"], w["B"], w["sigma"]
     n = n_of(w)
     Pl = P / L * np.ones(L)

@@ -61,10 +61,13 @@ def synth_y(op, Pl, sigma, seeds):
     return op.Ab_batch(beta0) + noise
 
 
-def sec_bytes(L, M, n, w, B, G, s):
-    """Algorithmic bytes of one k_sec launch: the two uint16
-    tables once, z once per codeword, β read + write, Ab partials written."""
-    return 2 * L * (w + n) + B * (n * s + 2 * L * M * s + G * n * s)
+def sec_bytes(L, M, n, w, B, G, s, kernel="k_sec4"):
+    """Algorithmic bytes of one k_sec launch: the bucket and Ab
+    tables once (uint16 per slot and per section-row; k_sec43 packs a section
+    triple's Ab entries into one uint32 per row), z once per codeword, β read
+    + write, Ab partials written."""
+    fwd = 4 * n * G if kernel == "k_sec43" else 2 * L * n
+    return 2 * L * w + fwd + B * (n * s + 2 * L * M * s + G * n * s)
 
 
 def row_bytes(n, B, G, s):
@@ -223,7 +226,7 @@ def main():
         G = plan["partials"]  # Ab partials per codeword of the section kernel this batch runs
         wv = op.w
         per = {
-            "k_sec": sec_bytes(L, M, n, wv, B, G, s),
+            "k_sec": sec_bytes(L, M, n, wv, B, G, s, plan["section_kernel"]),
             "k_row": row_bytes(n, B, G, s),
         }
     else:

@@ -105,6 +105,8 @@ int sa_stage_power_batch(sa_ctx* ctx, int B, const double* Pl);
 int sa_run(sa_ctx* ctx, int B, int T, int flags);
 int sa_wait(sa_ctx* ctx);
 int sa_fetch(sa_ctx* ctx, int B, double* beta_out, int* iters_out);
+/* The residual z of the last decode's final iteration, B x n (diagnostics). */
+int sa_fetch_z(sa_ctx* ctx, int B, double* z_out);
 double sa_run_event_ms(sa_ctx* ctx);
 
 /* Per-kernel device time of one EAGER decode of the staged batch (every

@@ -35,7 +35,7 @@ SA_PTR_DEVICE = 0x200
 # Every symbol include/sparc_amp.h declares (tests check the export table).
 EXPORTS = (
     "sa_create", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
-    "sa_reserve", "sa_stage", "sa_stage_power_batch", "sa_run", "sa_wait", "sa_fetch", "sa_run_event_ms",
+    "sa_reserve", "sa_stage", "sa_stage_power_batch", "sa_run", "sa_wait", "sa_fetch", "sa_fetch_z", "sa_run_event_ms",
     "sa_profile", "sa_profile_rep", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
     "sa_threshold", "sa_cancel", "sa_plan",
@@ -57,6 +57,7 @@ _SIG = {
     "sa_run": (_I, [_P, _I, _I, _I]),
     "sa_wait": (_I, [_P]),
     "sa_fetch": (_I, [_P, _I, _D, ct.POINTER(ct.c_int)]),
+    "sa_fetch_z": (_I, [_P, _I, _D]),
     "sa_run_event_ms": (ct.c_double, [_P]),
     "sa_profile": (_I, [_P, _I, _I, _I, _D]),
     "sa_profile_rep": (_I, [_P, _I, _I, _I, _I, _D]),

@@ -394,6 +394,7 @@ struct SecArgs {
   const uint16_t* __restrict__ inv;  // [L][w]  row of ordering value o, or n (zero slot)
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
+  const uint32_t* __restrict__ fwd3; // [ceil(L/3)][n] a section triple, 10-bit fields k | sign<<9 (M <= 512)
   const real* __restrict__ c;        // [L] sqrt(n * Pl), or [B][L] per codeword (cst = L)
   const real* __restrict__ z;        // [B][n]
   real* __restrict__ beta;           // [B][L*M] previous estimate (read)
@@ -466,11 +467,23 @@ __device__ __forceinline__ bool stage_z_dma(const real* zb, real* zs, int n, int
   const int lane = tid & 63, nbytes = n * (int)sizeof(real);
   for (int ch = tid >> 6; ch * 1024 < nbytes; ch += NT / 64) {
     const int off = ch * 1024 + lane * 16;
-    if (off < nbytes)
+    // whole 16-B pieces only: a piece straddling the end would land z's
+    // neighbour in the zero slot zs[n] (any wave's DMA may land after
+    // finish_z_dma's store); the tail goes through finish_z_dma
+    if (off + 16 <= nbytes)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)zb + off),
                                        (__attribute__((address_space(3))) void*)((char*)zs + ch * 1024), 16, 0, 0);
   }
   return true;
+}
+
+// After stage_z_dma: the < 16-B tail of z by ordinary loads, and the zero
+// slot zs[n] (gathered for empty buckets).
+template <typename real>
+__device__ __forceinline__ void finish_z_dma(const real* zb, real* zs, int n, int tid) {
+  const int n0 = n * (int)sizeof(real) / 16 * 16 / (int)sizeof(real);
+  if (tid < n - n0) zs[n0 + tid] = zb[n0 + tid];
+  if (tid == 0) zs[n] = 0;
 }
 
 template <int E, int KH>
@@ -632,7 +645,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     }
     STAMP(1);
     if (!dma) zst.store(zs, zb, n, tid);
-    else if (tid == 0) zs[n] = 0;
+    else finish_z_dma(zb, zs, n, tid);
     __syncthreads();
   STAMP(2);
 
@@ -825,7 +838,7 @@ __global__ void __launch_bounds__(256) k_sec2(SecArgs<real> a) {
   const real tau2 = tau * tau;
   STAMP(1);
   if (!dma) zst.store(zs, zb, n, tid);
-  else if (tid == 0) zs[n] = 0;
+  else finish_z_dma(zb, zs, n, tid);
   __syncthreads();
   STAMP(2);
 
@@ -973,11 +986,12 @@ __device__ __forceinline__ real combine_q(const real* red, int w0, int f) {
   return x[0];
 }
 
-template <typename real, int EQ, int QW>
+template <typename real, int EQ, int QW, int SPW = 2>
 __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
+  static_assert(SPW == 2 || SPW == 3, "sections per workgroup");
   STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NT = 2 * QW * 64;
+  constexpr int NT = SPW * QW * 64;
   constexpr int KH = EQ >= 8 ? 4 : 16;
   constexpr int NQ = (EQ + 3) / 4;
   constexpr int KR = (4608 + NT - 1) / NT;  // rows per thread per pass: n <= 4608 in one pass
@@ -986,23 +1000,23 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   const int sidx = wv / QW, q = wv % QW;
   const int M = a.M, n = a.n, Mq = M / QW;
   const size_t LM = (size_t)a.L * M;
-  const int l = g * 2 + sidx;
+  const int l = g * SPW + sidx;
   const bool have = l < a.L;
   const int lc = have ? l : a.L - 1;
   const int eoff = q * Mq;
 
   real* zs = reinterpret_cast<real*>(smem);
   const int zslots = ((n + 1) * (int)sizeof(real) + 15) / 16 * 16 / (int)sizeof(real);
-  real* ts = zs + zslots;          // [2][M]   T_l = H_M beta_l
-  real* xb = ts + 2 * M;           // [2][M]   top-stage exchange, one M per section
-  real* red = xb + 2 * M;          // [2*QW][4] per-wave max, S, S2, beta^2
+  real* ts = zs + zslots;          // [SPW][M]   T_l = H_M beta_l
+  real* xb = ts + SPW * M;         // [SPW][M]   top-stage exchange, one M per section
+  real* red = xb + SPW * M;        // [SPW*QW][4] per-wave max, S, S2, beta^2
 
   real v[EQ];
   real bprev[EQ];
   const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
   real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
   const uint16_t* il = a.inv + (size_t)lc * a.w + eoff;
-  const uint32_t* fw = a.fwd2 + (size_t)g * n;
+  const uint32_t* fw = (SPW == 2 ? a.fwd2 : a.fwd3) + (size_t)g * n;
   ushort4 tb[KH][NQ];
   uint32_t f[KR];
 
@@ -1037,7 +1051,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   const real tau2 = tau * tau;
   STAMP(1);
   if (!dma) zst.store(zs, zb, n, tid);
-  else if (tid == 0) zs[n] = 0;
+  else finish_z_dma(zb, zs, n, tid);
   __syncthreads();
   STAMP(2);
 #ifdef SA_STAMPS
@@ -1112,8 +1126,12 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   if (lane == 0) red[wv * 4 + 3] = bb;
   __syncthreads();
   STAMP(7);
-  if (tid == 0) a.bbp[(size_t)b * a.G + g] = red[0 * 4 + 3] + red[QW * 4 + 3];
-  // Ab partial of the pair for every row
+  if (tid == 0) {
+    real bsum = red[0 * 4 + 3] + red[QW * 4 + 3];
+    if constexpr (SPW == 3) bsum += red[2 * QW * 4 + 3];
+    a.bbp[(size_t)b * a.G + g] = bsum;
+  }
+  // Ab partial of the pair (triple) for every row
   real* abp = a.abp + ((size_t)b * a.G + g) * n;
   for (int r0 = 0; r0 < n; r0 += NT * KR) {
     if (r0 > 0) {  // n > NT * KR only
@@ -1128,10 +1146,20 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
       const int r = r0 + u * NT + tid;
       if (r < n) {
         const uint32_t e = f[u];
-        const real v0 = ts[e & 0x7fffu];
-        const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
-        real t = (e & 0x8000u) ? -v0 : v0;
-        t += (e & 0x80000000u) ? -v1 : v1;
+        real t;
+        if constexpr (SPW == 2) {
+          const real v0 = ts[e & 0x7fffu];
+          const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
+          t = (e & 0x8000u) ? -v0 : v0;
+          t += (e & 0x80000000u) ? -v1 : v1;
+        } else {
+          const real v0 = ts[e & 0x1ffu];
+          const real v1 = ts[M + ((e >> 10) & 0x1ffu)];
+          const real v2 = ts[2 * M + ((e >> 20) & 0x1ffu)];
+          t = (e & 0x200u) ? -v0 : v0;
+          t += (e & 0x80000u) ? -v1 : v1;
+          t += (e & 0x20000000u) ? -v2 : v2;
+        }
         st_part(&abp[r], t);
       }
     }
@@ -1145,6 +1173,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
 
 template <typename real, int E4>
 __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) { secq_body<real, E4, 4>(a); }
+// Three sections per workgroup (12 waves): L = 3 x CUs (L = 768 on 256 CUs)
+// puts one workgroup on every CU where pairs leave half the CUs with two.
+template <typename real, int E4>
+__global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real, E4, 4, 3>(a); }
 // ---------------------------------------------------------------------------
 // Batched section kernel (B codewords share the operator)
 // ---------------------------------------------------------------------------
@@ -1978,6 +2010,10 @@ struct sa_ctx {
   size_t lda = 0;
   size_t sec_lds = 0;
   int G2 = 0;          // k_sec2 pairs of sections (0: k_sec2 unavailable)
+  int G3 = 0;          // k_sec43 triples of sections (used when sec3)
+  bool sec3 = false;   // k_sec43 (three sections x 4 waves per workgroup) chosen over k_sec4
+  size_t sec3_lds = 0;
+  uint32_t* d_fwd3 = nullptr;
   bool sec4 = false;   // k_sec4 (4 waves per section) fits and is chosen
   size_t sec4_lds = 0;
   int NZ16 = 0;        // k_row2 16-row blocks; nz_cur = z^2 partial count of the current decode
@@ -2066,6 +2102,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   int Gmax = c->G > c->KS ? c->G : c->KS;
   if (c->Gb > Gmax) Gmax = c->Gb;
   if (c->G2 > Gmax) Gmax = c->G2;
+  if (c->G3 > Gmax) Gmax = c->G3;
   int rc;
   if ((rc = dev_alloc(c, &c->d_y, nB * c->n * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_z, nB * c->n * s))) return rc;
@@ -2142,7 +2179,7 @@ int download(sa_ctx* c, double* dst, const void* src, size_t count) {
 template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
-  a.inv = c->d_inv; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.c = (const real*)c->d_c;
+  a.inv = c->d_inv; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
@@ -2240,14 +2277,27 @@ bool use_sec2(const sa_ctx* c, int B) {
          !getenv("SPARC_AMP_NO_SEC2");
 }
 
+// Ab / beta^2 partials per codeword of the unbatched multi-wave section kernels
+int sec2_parts(const sa_ctx* c) { return c->sec3 ? c->G3 : c->G2; }
+
 template <typename real>
 int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout) {
   SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
   a.beta = (real*)bin;
   a.beta_out = (real*)bout;
-  a.G = c->G2;
-  dim3 grid(c->G2, B);
+  a.G = sec2_parts(c);
+  dim3 grid(a.G, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
+  if (c->sec3) {
+    switch (c->M / 256) {
+      case 1: PROF_REPS(c) k_sec43<real, 1><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
+      case 2: PROF_REPS(c) k_sec43<real, 2><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
+      default: return fail(SA_ERR_UNSUPPORTED, "k_sec43: M");
+    }
+    if (c->prof) c->prof->end(c->stream);
+    HIP_TRY(hipGetLastError());
+    return SA_OK;
+  }
   if (c->sec4) {
     switch (c->M / 256) {
       case 1: PROF_REPS(c) k_sec4<real, 1><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
@@ -2408,8 +2458,8 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const bool sec2 = use_sec2(c, B);
   c->nz_cur = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;  // z^2 partials: k_row2 or k_row blocks
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
-  const int G = dense ? c->KS : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
-  const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
+  const int G = dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
+  const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
   int rc;
   k_fill32<<<(B + 255) / 256, 256, 0, c->stream>>>((uint32_t*)c->d_iters, 0xffffffffu, (size_t)B);
   if (has_b0) {
@@ -2572,6 +2622,7 @@ int build_tables(sa_ctx* c) {
   const int G = (L + kSG - 1) / kSG * (kSG / kSpw);  // padded to whole batched groups
   std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);  // [G][n][4]; missing sections -> (k 0, +)
   std::vector<uint32_t> fwd2((size_t)((L + 1) / 2) * n, 0);  // [L/2][n] section pairs
+  std::vector<uint32_t> fwd3(c->sec3 ? (size_t)c->G3 * n : 0, 0);  // [L/3][n] section triples
   for (int l = 0; l < L; ++l) {
     const uint32_t* o = c->ordering.data() + (size_t)l * n;
     uint16_t* il = inv.data() + (size_t)l * w;
@@ -2587,18 +2638,23 @@ int build_tables(sa_ctx* c) {
       const uint16_t e = (uint16_t)((v & (uint32_t)(M - 1)) | ((__builtin_popcount(hi) & 1u) << 15));
       fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)] = e;
       fwd2[(size_t)(l / 2) * n + r] |= (uint32_t)e << (16 * (l & 1));
+      if (c->sec3)  // M <= 512: k in 9 bits, the sign in bit 9 of a 10-bit field
+        fwd3[(size_t)(l / 3) * n + r] |= (uint32_t)((e & 0x1ffu) | ((e >> 15) << 9)) << (10 * (l % 3));
     }
   }
   int rc;
   if ((rc = dev_alloc(c, (void**)&c->d_inv, inv.size() * 2))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_fwd, fwd.size() * 2))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_fwd2, fwd2.size() * 4))) return rc;
+  if (c->sec3 && (rc = dev_alloc(c, (void**)&c->d_fwd3, fwd3.size() * 4))) return rc;
   // On the context's (non-blocking) stream and waited for: a pageable
   // hipMemcpy may return once the data is staged, before the DMA lands, and
   // the null stream does not order the kernels of a non-blocking stream.
   HIP_TRY(hipMemcpyAsync(c->d_inv, inv.data(), inv.size() * 2, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_fwd, fwd.data(), fwd.size() * 2, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->d_fwd2, fwd2.data(), fwd2.size() * 4, hipMemcpyHostToDevice, c->stream));
+  if (c->sec3)
+    HIP_TRY(hipMemcpyAsync(c->d_fwd3, fwd3.data(), fwd3.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
@@ -2632,6 +2688,7 @@ hipError_t lds_attr_all() {
   SA_A((k_sec2<real, 16>)) SA_A((k_sec2<real, 32>))
   SA_A((k_sec4<real, 1>)) SA_A((k_sec4<real, 2>)) SA_A((k_sec4<real, 4>)) SA_A((k_sec4<real, 8>))
   SA_A((k_sec4<real, 16>))
+  SA_A((k_sec43<real, 1>)) SA_A((k_sec43<real, 2>))
   SA_A((k_secb<real, 1, 1, kWB>)) SA_A((k_secb<real, 2, 1, kWB>)) SA_A((k_secb<real, 4, 1, kWB>))
   SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
   SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
@@ -2740,6 +2797,21 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       c->n_cus = prop.multiProcessorCount;
   }
   c->Gd = (L + 3) / 4;
+  {
+    // k_sec43: three sections per workgroup where pairs overfill the chip
+    // (ceil(L/2) > CUs >= ceil(L/3), e.g. L = 768) — one workgroup per CU
+    // instead of two on half of them; SPARC_AMP_SEC3=0/1 forces it off/on
+    const size_t need3 = (((size_t)(n + 1) * s + 15) / 16 * 16) + 6 * (size_t)M * s + 48 * s;
+    const char* e3 = getenv("SPARC_AMP_SEC3");
+    const int G3 = (L + 2) / 3;
+    const bool fits = c->sec4 && backend == SA_BACKEND_HADAMARD && M <= 512 && need3 <= 160 * 1024;
+    const bool want = e3 ? e3[0] == '1' : (c->G2 > c->n_cus && G3 <= c->n_cus);
+    if (fits && want) {
+      c->sec3 = true;
+      c->G3 = G3;
+      c->sec3_lds = need3;
+    }
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
     delete c;
@@ -3041,6 +3113,7 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_inv);
   dev_free(c->d_fwd);
   dev_free(c->d_fwd2);
+  dev_free(c->d_fwd3);
   dev_free(c->d_A);
   dev_free(c->d_c);
   dev_free(c->d_cd);
@@ -3144,6 +3217,16 @@ double sa_run_event_ms(sa_ctx* c) {
   float ms = -1.f;
   if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.0;
   return ms;
+}
+
+int sa_fetch_z(sa_ctx* c, int B, double* z_out) {
+  if (check_ctx(c) || !z_out) return fail(SA_ERR_ARG, "sa_fetch_z: bad arguments");
+  if (B <= 0 || B > c->Bcap) return fail(SA_ERR_ARG, "sa_fetch_z: bad batch");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = download(c, z_out, c->d_z, (size_t)B * c->n))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
 }
 
 int sa_fetch(sa_ctx* c, int B, double* beta_out, int* iters_out) {
@@ -3395,14 +3478,14 @@ int sa_plan(sa_ctx* c, int B, int64_t* o) {
   const bool dense = c->backend == SA_BACKEND_DENSE;
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
-  o[0] = dense ? 3 : (batched ? 2 : (sec2 ? (c->sec4 ? 4 : 1) : 0));
-  o[1] = dense ? c->KS : (batched ? c->Gb : (sec2 ? c->G2 : c->G));
+  o[0] = dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? 5 : (c->sec4 ? 4 : 1)) : 0));
+  o[1] = dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
   o[3] = batched ? c->CB : 1;
   o[4] = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;
   o[5] = c->w;
   o[6] = B * c->NZ < 4 * c->n_cus ? 1 : 0;
-  o[7] = 0;
+  o[7] = c->n_cus;
   return SA_OK;
 }
 

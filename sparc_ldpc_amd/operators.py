@@ -215,7 +215,13 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, dptr(out), iters.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return out, iters
 
-    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4")
+    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43")
+
+    def fetch_z(self, B):
+        """Residual z after the last decode's final iteration, (B, n)."""
+        z = np.empty((B, self.n))
+        check(self._lib.sa_fetch_z(self._ctx, int(B), z.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_double))))
+        return z
 
     def plan(self, B):
         """Which kernels a decode of B codewords runs (sa_plan)."""
@@ -223,7 +229,7 @@ class SparcOperator:
         check(self._lib.sa_plan(self._ctx, int(B), o.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int64))))
         return dict(section_kernel=self.SECTION_KERNELS[int(o[0])], partials=int(o[1]), row_splits=int(o[2]),
                     codewords_per_wg=int(o[3]), zz_partials=int(o[4]), w=int(o[5]),
-                    row_kernel="k_row2" if o[6] else "k_row")
+                    row_kernel="k_row2" if o[6] else "k_row", cus=int(o[7]))
 
     def info(self):
         o = np.zeros(8, dtype=np.int64)

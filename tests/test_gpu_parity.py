@@ -358,6 +358,50 @@ def test_maximum_sizes_vs_oracle(sp, prec, L, M, n):
         sp.SparcOperator(2, 8, 65535, sp.make_ordering(2, 8, 65535), precision=prec)
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+@pytest.mark.parametrize("L,M,n", [(258, 512, 2580), (257, 256, 2284), (300, 512, 6000)])
+def test_triple_section_kernel(sp, prec, L, M, n, monkeypatch):
+    """k_sec43 (three sections per workgroup, chosen by default for L = 768 on
+    256 CUs) forced on, incl. a missing third section (L % 3 != 0) and n past
+    one row pass (n > 4608): against the oracle per iteration and against the
+    pair kernel k_sec4."""
+    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
+    Pl = 2.0 / L * np.ones(L)
+    ys = [orc.rep_inputs(L, M, n, Pl, 0.9, oAb, 300 + i)[1].reshape(-1) for i in range(2)]
+    ops = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SPARC_AMP_SEC3", flag)
+        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
+    monkeypatch.delenv("SPARC_AMP_SEC3")
+    assert ops["1"].plan(1)["section_kernel"] == "k_sec43"
+    assert ops["1"].plan(1)["partials"] == (L + 2) // 3
+    assert ops["0"].plan(1)["section_kernel"] == "k_sec4"
+    for y in ys:
+        for t in (1, 2, 5):
+            ref, _ = orc.amp_test(y, 0, Pl, L, M, t, oAb, oAz)
+            b3, _ = ops["1"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+            b2, _ = ops["0"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+            assert rel(b3[0], ref) <= TOL[prec], t
+            assert rel(b3[0], b2[0]) <= 2 * TOL[prec], t
+        b3, i3 = ops["1"].amp_batch(y.reshape(1, -1), Pl, 30)
+        b3b, i3b = ops["1"].amp_batch(y.reshape(1, -1), Pl, 30)
+        assert np.array_equal(b3, b3b) and np.array_equal(i3, i3b)  # bitwise reproducible
+        assert argmax_agree(b3[0], orc.amp(y, 0, Pl, L, M, 30, oAb, oAz), L, M)
+
+
+def test_c4_single_uses_triples(sp):
+    """L=768 M=512 R=5/6 (n=8294) single codeword: the triple kernel is the
+    default where pairs overfill the chip (ceil(L/2) > CUs >= ceil(L/3))."""
+    L, M = 768, 512
+    n = int(L * np.log2(M) / (5 / 6))
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n))
+    plan = op.plan(1)
+    cus = plan["cus"]
+    want = "k_sec43" if (L + 1) // 2 > cus >= (L + 2) // 3 else "k_sec4"
+    assert plan["section_kernel"] == want
+    assert plan["partials"] == (256 if want == "k_sec43" else 384)
+
+
 @pytest.mark.parametrize("B", [1, 6])
 def test_profile_rep_and_plan(sp, B):
     """sa_profile / sa_profile_rep (the bench's roofline timing): positive

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("k_secb", "k_sec2", "k_sec4", "k_sec8", "k_sec", "k_row2", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide",
+    for k in ("k_secb", "k_sec2", "k_sec43", "k_sec4", "k_sec8", "k_sec", "k_row2", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide",
               "k_bp", "k_llr", "k_bp2sp", "k_sp_norm", "k_colsum"):
         if any(p in name for p in (f"::{k}<", f" {k}<", f" {k}(", f"::{k}(")) or name.startswith((f"{k}<", f"{k}(")):
             return k

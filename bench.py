@@ -81,33 +81,68 @@ def gemv_bytes(L, M, n):
 
 
 def _cpu_worker(args):
+    """One host process: build the oracle operator (untimed), then time Tsample
+    AMP iterations of one codeword; returns the wall-clock span."""
     L, M, n, P, sigma, Tsample, seed = args
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import amp_oracle as orc
     Ab, Az, _ = orc.sparc_transforms(L, M, n)
     Pl = P / L * np.ones(L)
     _, y = orc.rep_inputs(L, M, n, Pl, sigma, Ab, seed)
-    t0 = time.perf_counter()
+    t0 = time.time()
     orc.amp(y, sigma, Pl, L, M, Tsample, Ab, Az)
-    return (time.perf_counter() - t0) / Tsample
+    return t0, time.time()
 
 
-def cpu_baseline(w, procs, Tsample=4):
-    """The oracle (reference algorithm in fp64 NumPy, vectorised FWHT) on the
-    host cores: `procs` independent processes, each timing Tsample AMP
-    iterations of one codeword; extrapolated to T iterations per codeword."""
+def host_cpus():
+    """(usable cores, description): every core of sched_getaffinity, bounded by
+    the cgroup CPU quota when one is set (the cores this process may really
+    use), and the CPU model from /proc/cpuinfo."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    use = aff if quota is None else min(aff, quota)
+    return use, f"{model}; sched_getaffinity {aff} cores, cgroup quota {quota or 'none'}"
+
+
+def cpu_baseline(w, procs=None, Tsample=None):
+    """The oracle (the reference's algorithm in fp64 NumPy, vectorised FWHT) on
+    the host: `procs` independent single-threaded processes (default: every
+    usable core), each timing Tsample AMP iterations of its own codeword; the
+    rate is all iterations over the wall-clock span from the first start to
+    the last finish, scaled to T iterations per codeword."""
     import multiprocessing as mp
     L, M, P, sigma, T = w["L"], w["M"], w["P"], w["sigma"], w["T"]
     n = n_of(w)
+    use, desc = host_cpus()
+    procs = procs or use
+    Tsample = Tsample or T  # a whole decode per process: no extrapolation
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs) as pool:
-        per_iter = pool.map(_cpu_worker, [(L, M, n, P, sigma, Tsample, 1000 + i) for i in range(procs)])
-    sec_per_cw = float(np.mean(per_iter)) * T
+        spans = pool.map(_cpu_worker, [(L, M, n, P, sigma, Tsample, 1000 + i) for i in range(procs)])
+    wall = max(e for _, e in spans) - min(s for s, _ in spans)
+    per_core = float(np.mean([e - s for s, e in spans])) / Tsample
     return {
-        "value": procs / sec_per_cw, "unit": "codewords/s", "cores": procs, "kind": "port",
-        "sample": f"oracle amp() fp64 NumPy, {procs} procs x 1 codeword x {Tsample} iterations "
-                  f"(L={L} M={M} n={n}), extrapolated to T={T} iterations/codeword; "
-                  f"{np.mean(per_iter) * 1e3:.1f} ms/iteration/core",
+        "value": procs * Tsample / wall / T, "unit": "codewords/s", "cores": procs, "kind": "port",
+        "cpu": desc,
+        "sample": f"oracle amp() fp64 NumPy (the reference algorithm), {procs} single-threaded processes x "
+                  f"1 codeword x {Tsample} iterations (L={L} M={M} n={n}) in {wall:.1f} s wall, "
+                  f"scaled to T={T} iterations/codeword; {per_core * 1e3:.1f} ms/iteration/process",
     }
 
 
@@ -155,26 +190,20 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0)
+    ap.add_argument("--no-fp64", action="store_true", help="skip the binary64 leg of an fp32 run")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # SPARC_BENCH_DIST=gloo: rehearsal of the N-rank path on a box with fewer
-    # GPUs than ranks (ranks share device LOCAL_RANK % device_count); the
-    # driver's multi-GPU runs use the default, RCCL with one GPU per rank
-    backend = os.environ.get("SPARC_BENCH_DIST", "nccl")
-    device = local
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        if backend != "nccl":
-            device = local % torch.cuda.device_count()
-        torch.cuda.set_device(device)
-        dist.init_process_group(backend)  # "nccl" = RCCL over xGMI
-
     import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd import dist
+
+    rank, world, local = dist.env_rank()
+    # one rank per GPU over RCCL (librccl through ctypes, no PyTorch); the
+    # rehearsal mode SPARC_DIST_BACKEND=socket puts several ranks on one GPU
+    # (device LOCAL_RANK % device count) with the CPU all-reduce instead
+    ndev = sp.load_library().sa_device_count()
+    device = local % max(1, ndev) if os.environ.get("SPARC_DIST_BACKEND") == "socket" else local
+    if world > 1:
+        dist.init(device=device)
 
     w = dict(WORKLOADS[args.workload])
     if args.batch and args.batch != w["B"]:
@@ -193,10 +222,7 @@ def main():
 
     def sync_all():
         op.wait()
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        dist.barrier()
 
     for _ in range(args.warmup):
         op.run(B, T, early_stop=False)
@@ -206,11 +232,7 @@ def main():
         op.run(B, T, early_stop=False)
     sync_all()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}" if backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = float(dist.allreduce_max(np.array([elapsed]))[0])  # the slowest rank's time
 
     # per-kernel device times over one eager decode (HIP events on the
     # library's stream), for the roofline of the dominant kernel
@@ -251,7 +273,7 @@ def main():
     }
 
     result = {
-        "metric": "decoded codewords/sec (T AMP iters) at L=512,M=512; achieved HBM GB/s vs roofline",
+        "metric": f"decoded codewords/sec (T AMP iters) at L={L},M={M}; achieved HBM GB/s vs roofline",
         "value": round(B * args.steps * world / elapsed, 3),
         "unit": "codewords/s",
         "n_gpus": world,
@@ -268,19 +290,38 @@ def main():
                    "early_stop": False, "parallelism": f"reps sharded over {world} GPU(s)"},
         "roofline": roofline,
     }
+    if args.precision == "fp32" and args.backend == "hadamard" and not args.no_fp64:
+        # the same workload in binary64 (the reference's precision; the joint
+        # decoder's): same seeds, same timing protocol, every rank
+        op64 = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="hadamard", precision="fp64",
+                                device=device)
+        op64.reserve(B, T)
+        op64.stage(y, Pl)
+        for _ in range(args.warmup):
+            op64.run(B, T, early_stop=False)
+        op64.wait()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            op64.run(B, T, early_stop=False)
+        op64.wait()
+        dist.barrier()
+        e64 = float(dist.allreduce_max(np.array([time.perf_counter() - t0]))[0])
+        result["fp64_leg"] = {"value": round(B * args.steps * world / e64, 3), "unit": "codewords/s",
+                              "ms_per_step": round(e64 / args.steps * 1e3, 4), "dtype": "f64",
+                              "section_kernel": op64.plan(B)["section_kernel"]}
+        del op64
     if rank == 0 and world == 1 and not args.no_dense:
         try:
             result["dense_gemv"] = dense_gemv_probe(device)
         except Exception as e:  # report, never hide
             result["dense_gemv"] = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu:
-        procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
-        result["cpu_baseline"] = cpu_baseline(w, procs)
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_procs or None)
         result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    dist.finalize()
 
 
 if __name__ == "__main__":

@@ -142,6 +142,11 @@ int sa_encode(sa_ctx* ctx, int B, const int32_t* idx, const double* noise);
  * with c_l at idx[b][l] (B x L) for the next sa_run(..., SA_FLAG_BETA0). */
 int sa_stage_onehot(sa_ctx* ctx, int B, const int32_t* idx);
 
+/* The same with amplitude scale * c_l, idx -1 = an all-zero section: the 0/1
+ * start beta_0 = beta / sqrt(n P / L) with its first L_zero sections zeroed of
+ * the amp_test.py reps loop (amp_test.py:202-204; scale = 1 / sqrt(n P / L)). */
+int sa_stage_onehot_scaled(sa_ctx* ctx, int B, const int32_t* idx, double scale);
+
 /* sp2bp + LLR (sparc_ldpc.py:470-479, :257-281) of sections [l0, l0+ns) of
  * the current beta: llr = nan_to_num(log(1-p) - log(p)), p the bitwise
  * posterior of beta_l / c_l. */
@@ -170,6 +175,11 @@ int sa_threshold(sa_ctx* ctx, int B, int l0, int ns, const double* app, int flag
  * not cancelled; dst is a context over the same n (e.g. sa_subset of the
  * undecided sections). */
 int sa_cancel(sa_ctx* ctx, int B, const int32_t* idx, sa_ctx* dst);
+
+/* The same with beta(idx) at amplitude scale * c_l: y - Ab(beta_0) of the
+ * amp_test.py reps loop's hard initialisation (amp_test.py:207-210), where
+ * beta_0 carries 1 = c_l / sqrt(n P / L) at the decided sections. */
+int sa_cancel_scaled(sa_ctx* ctx, int B, const int32_t* idx, double scale, sa_ctx* dst);
 
 /* Introspection. */
 /* The kernels a decode of B codewords runs: out8 = {section kernel (0 k_sec,

@@ -1555,8 +1555,12 @@ struct RowArgs {
   const real* __restrict__ tau;  // [B][T1]
   real* __restrict__ out;        // [B][n] (ROW_ABOUT)
   int n, G, Gb, NZ, T1, t, mode, early_stop;  // G Ab partials, Gb beta^2 partials
-  real sqrt_n, P;
-  const real* __restrict__ Pb;   // [B] per-codeword P (sa_stage_power_batch), or null: P
+  real sqrt_n;
+  // total power P = sum(Pl) read from device memory (never a captured
+  // argument: a graph replayed after set_power must see the new P):
+  // [B] per codeword (sa_stage_power_batch, Pbst = 1) or one shared value (Pbst = 0)
+  const real* __restrict__ Pb;
+  int Pbst;
 };
 
 // Residual update with the Onsager term (sparc_ldpc.py:220):
@@ -1615,7 +1619,7 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   real ons = 0;
   if (a.mode == ROW_AMP) {
     const real bb = a.Gb <= 128 ? wave_sum_pair(bbv[0], bbv[1]) : wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
-    ons = (a.Pb ? a.Pb[b] : a.P) - bb / (real)n;
+    ons = a.Pb[(size_t)b * a.Pbst] - bb / (real)n;
   }
   real zn = 0;
   if (r < n) {
@@ -1704,7 +1708,7 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
     } else {
       bb = wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
     }
-    ons = (a.Pb ? a.Pb[b] : a.P) - bb / (real)n;
+    ons = a.Pb[(size_t)b * a.Pbst] - bb / (real)n;
   }
   real zn = 0;
   if (tid < kRow2Rows && r < n) {
@@ -2042,6 +2046,7 @@ struct sa_ctx {
   // per-codeword power allocation (sa_stage_power_batch): c [Bcap][L], P [Bcap]
   void* d_cb = nullptr;
   void* d_Pb = nullptr;
+  void* d_P1 = nullptr;  // the shared P = sum(Pl) of set_power (one `real`)
   bool pb_on = false;
   bool shared_power = false;  // sa_stage's Pl staged (c_l of the binary64 glue kernels)
   size_t bytes = 0;
@@ -2204,8 +2209,8 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb
   a.early_stop = early_stop;
   // the dense matrix already carries the 1/sqrt(n) of sparc_ldpc.py:143-146
   a.sqrt_n = c->backend == SA_BACKEND_DENSE ? (real)1 : (real)std::sqrt((double)c->n);
-  a.P = (real)c->P;
-  a.Pb = c->pb_on ? (const real*)c->d_Pb : nullptr;
+  a.Pb = c->pb_on ? (const real*)c->d_Pb : (const real*)c->d_P1;
+  a.Pbst = c->pb_on ? 1 : 0;
   return a;
 }
 
@@ -2576,6 +2581,7 @@ int set_power(sa_ctx* c, const double* Pl) {
   }
   c->P = P;
   int rc = upload(c, c->d_c, cl.data(), c->L);
+  if (!rc) rc = upload(c, c->d_P1, &P, 1);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(c->d_cd, cl.data(), (size_t)c->L * 8, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));  // cl is a host temporary
@@ -2828,6 +2834,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   }
   if (!rc) rc = dev_alloc(c, &c->d_c, (size_t)L * s);
   if (!rc) rc = dev_alloc(c, (void**)&c->d_cd, (size_t)L * 8);
+  if (!rc) rc = dev_alloc(c, &c->d_P1, s);
   if (rc) {
     sa_destroy(c);
     return rc;
@@ -2872,7 +2879,7 @@ template <typename real>
 __global__ void __launch_bounds__(256) k_colsum(const ushort4* __restrict__ fwd, const double* __restrict__ cd,
                                                 const int32_t* __restrict__ idx, int ldi, int l0, int ns,
                                                 const real* __restrict__ base, const double* __restrict__ add,
-                                                real* __restrict__ out, int n, double sqrt_n) {
+                                                real* __restrict__ out, int n, double sqrt_n, double amp) {
   extern __shared__ int32_t sidx[];
   const int b = blockIdx.y, r = blockIdx.x * 256 + threadIdx.x;
   for (int i = threadIdx.x; i < ns; i += 256) sidx[i] = idx[(size_t)b * ldi + i];
@@ -2892,7 +2899,7 @@ __global__ void __launch_bounds__(256) k_colsum(const ushort4* __restrict__ fwd,
       acc += neg ? -cd[l] : cd[l];
     }
   }
-  const double x = acc / sqrt_n;
+  const double x = (amp == 1.0 ? acc : acc * amp) / sqrt_n;
   const size_t o = (size_t)b * n + r;
   out[o] = base ? (real)((double)base[o] - x) : (real)(x + (add ? add[o] : 0.0));
 }
@@ -2997,12 +3004,12 @@ __global__ void k_app_idx(const double* __restrict__ app, int lgM, int ns, int B
 // One-hot beta0 (sparc_ldpc.py:832-835): beta[b][l*M + idx[b][l]] = c_l, 0 elsewhere.
 template <typename real>
 __global__ void k_onehot(const int32_t* __restrict__ idx, const double* __restrict__ cd, int L, int M, int B,
-                         real* __restrict__ beta) {
+                         double scale, real* __restrict__ beta) {
   const size_t tot = (size_t)B * L * M;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < tot; i += (size_t)gridDim.x * blockDim.x) {
     const size_t bl = i / M;
     const int m = (int)(i % M), l = (int)(bl % L);
-    beta[i] = m == idx[bl] ? (real)cd[l] : (real)0;
+    beta[i] = m == idx[bl] ? (real)(scale == 1.0 ? cd[l] : cd[l] * scale) : (real)0;  // idx < 0: all zero
   }
 }
 
@@ -3073,10 +3080,10 @@ int dev_in(sa_ctx* c, const double* p, size_t count, int flags, const double** o
 
 template <typename real>
 int launch_colsum(sa_ctx* c, const int32_t* d_idx, int ldi, int l0, int ns, const real* base, const double* add,
-                  real* out, int B) {
+                  real* out, int B, double amp = 1.0) {
   dim3 grid((c->n + 255) / 256, B);
   k_colsum<real><<<grid, 256, (size_t)ns * sizeof(int32_t), c->stream>>>(
-      (const ushort4*)c->d_fwd, c->d_cd, d_idx, ldi, l0, ns, base, add, out, c->n, std::sqrt((double)c->n));
+      (const ushort4*)c->d_fwd, c->d_cd, d_idx, ldi, l0, ns, base, add, out, c->n, std::sqrt((double)c->n), amp);
   HIP_TRY(hipGetLastError());
   return SA_OK;
 }
@@ -3117,6 +3124,7 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_A);
   dev_free(c->d_c);
   dev_free(c->d_cd);
+  dev_free(c->d_P1);
   dev_free(c->d_stage);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -3345,22 +3353,32 @@ int sa_encode(sa_ctx* c, int B, const int32_t* idx, const double* noise) {
   return SA_OK;
 }
 
-int sa_stage_onehot(sa_ctx* c, int B, const int32_t* idx) {
+namespace {
+int stage_onehot_impl(sa_ctx* c, int B, const int32_t* idx, double scale, bool allow_empty) {
   if (check_ctx(c)) return SA_ERR_ARG;
   if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_stage_onehot: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_stage_onehot: power allocation not staged");
+  if (!std::isfinite(scale)) return fail(SA_ERR_ARG, "sa_stage_onehot: scale must be finite");
   for (size_t i = 0; i < (size_t)B * c->L; ++i)
-    if (idx[i] < 0 || idx[i] >= c->M) return fail(SA_ERR_ARG, "sa_stage_onehot: index outside [0, M)");
+    if (idx[i] >= c->M || (idx[i] < 0 && !(allow_empty && idx[i] == -1)))
+      return fail(SA_ERR_ARG, "sa_stage_onehot: index outside [0, M)");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemcpyAsync(c->d_idx, idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   const size_t tot = (size_t)B * c->L * c->M;
   if (c->prec == SA_PREC_F64)
-    k_onehot<double><<<grid_of(tot), 256, 0, c->stream>>>(c->d_idx, c->d_cd, c->L, c->M, B, (double*)c->d_beta);
+    k_onehot<double><<<grid_of(tot), 256, 0, c->stream>>>(c->d_idx, c->d_cd, c->L, c->M, B, scale, (double*)c->d_beta);
   else
-    k_onehot<float><<<grid_of(tot), 256, 0, c->stream>>>(c->d_idx, c->d_cd, c->L, c->M, B, (float*)c->d_beta);
+    k_onehot<float><<<grid_of(tot), 256, 0, c->stream>>>(c->d_idx, c->d_cd, c->L, c->M, B, scale, (float*)c->d_beta);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
+}
+}  // namespace
+
+int sa_stage_onehot(sa_ctx* c, int B, const int32_t* idx) { return stage_onehot_impl(c, B, idx, 1.0, false); }
+
+int sa_stage_onehot_scaled(sa_ctx* c, int B, const int32_t* idx, double scale) {
+  return stage_onehot_impl(c, B, idx, scale, true);
 }
 
 int sa_llr(sa_ctx* c, int B, int l0, int ns, double* llr, int flags) {
@@ -3453,7 +3471,7 @@ int sa_threshold(sa_ctx* c, int B, int l0, int ns, const double* app, int flags,
   return SA_OK;
 }
 
-int sa_cancel(sa_ctx* c, int B, const int32_t* idx, sa_ctx* dst) {
+int sa_cancel_scaled(sa_ctx* c, int B, const int32_t* idx, double scale, sa_ctx* dst) {
   if (check_ctx(c) || check_ctx(dst)) return SA_ERR_ARG;
   if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_cancel: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_cancel: power allocation not staged");
@@ -3461,17 +3479,20 @@ int sa_cancel(sa_ctx* c, int B, const int32_t* idx, sa_ctx* dst) {
     return fail(SA_ERR_ARG, "sa_cancel: dst must share n, precision and device");
   for (size_t i = 0; i < (size_t)B * c->L; ++i)
     if (idx[i] >= c->M) return fail(SA_ERR_ARG, "sa_cancel: index >= M");
+  if (!std::isfinite(scale)) return fail(SA_ERR_ARG, "sa_cancel: scale must be finite");
   HIP_TRY(hipSetDevice(c->device));
   int rc;
   if ((rc = ensure_workspace(dst, B, dst->Tcap > 0 ? dst->Tcap : 1))) return rc;
   HIP_TRY(hipMemcpyAsync(c->d_idx, idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   rc = c->prec == SA_PREC_F64
-           ? launch_colsum<double>(c, c->d_idx, c->L, 0, c->L, (const double*)c->d_y, nullptr, (double*)dst->d_y, B)
-           : launch_colsum<float>(c, c->d_idx, c->L, 0, c->L, (const float*)c->d_y, nullptr, (float*)dst->d_y, B);
+           ? launch_colsum<double>(c, c->d_idx, c->L, 0, c->L, (const double*)c->d_y, nullptr, (double*)dst->d_y, B, scale)
+           : launch_colsum<float>(c, c->d_idx, c->L, 0, c->L, (const float*)c->d_y, nullptr, (float*)dst->d_y, B, scale);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
+
+int sa_cancel(sa_ctx* c, int B, const int32_t* idx, sa_ctx* dst) { return sa_cancel_scaled(c, B, idx, 1.0, dst); }
 
 int sa_plan(sa_ctx* c, int B, int64_t* o) {
   if (check_ctx(c) || !o || B <= 0) return fail(SA_ERR_ARG, "sa_plan: bad arguments");

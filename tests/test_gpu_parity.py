@@ -469,3 +469,95 @@ def test_amp_init_test(sp, capsys):
     assert b_init == [0.0] and b_no == [0.0]
     out = capsys.readouterr().out
     assert "For initialised amp, BER=  [0.0]" in out and "all zero beta_0" in out
+
+
+def test_c2_batch256_golden(sp):
+    """BASELINE configs[2] at its own batch size: 256 codewords of C2 in one
+    decode, which runs the batched section kernel k_secb and the 64-row k_row
+    over the whole grid (the launch shape of the c3 bench line).  Slot 0 holds
+    the golden y: t = 1 and the converged estimate against the reference's;
+    other slots (seeded reps) against the oracle at fixed t = 2."""
+    g = golden("c2.npz")
+    L, M, n, T = int(g["L"]), int(g["M"]), int(g["n"]), int(g["T"])
+    B = 256
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp32")
+    plan = op.plan(B)
+    assert plan["section_kernel"] == "k_secb" and plan["row_kernel"] == "k_row", plan
+    Pl = float(g["P"]) / L * np.ones(L)
+    oAb, oAz, _ = orc.sparc_transforms(L, M, n)
+    sigma = float(g["sigma"])
+    Y = np.empty((B, n))
+    Y[0] = g["y"].reshape(-1)
+    slots = (1, 77, 128, 255)
+    for s in range(1, B):
+        rs = np.random.RandomState(5000 + s)
+        b0 = np.zeros(L * M)
+        b0[np.arange(L) * M + rs.randint(0, M, L)] = np.sqrt(n * Pl)
+        Y[s] = rs.randn(n) * sigma  # noise; the codeword part added below
+        if s in slots:
+            Y[s] += oAb(b0).reshape(-1)
+        else:
+            Y[s] += op.Ab_batch(b0[None, :])[0]
+    b1, _ = op.amp_batch(Y, Pl, 1)
+    assert rel(b1[0], g["beta_t1"]) <= max(TOL["fp32"], 1e-7)
+    bf, it = op.amp_batch(Y, Pl, T)
+    assert rel(bf[0], g["beta_final"]) <= TOL["fp32"]
+    assert np.array_equal(orc.section_argmax(bf[0], L, M), g["argmax_final"])
+    assert np.all((it >= 0) & (it <= T))  # T: the loop ran out
+    b2, _ = op.amp_batch(Y, Pl, 2, early_stop=False)
+    for s in slots:
+        ref = orc.amp(Y[s], 0, Pl, L, M, 2, oAb, oAz)
+        assert rel(b2[s], ref) <= TOL["fp32"], s
+        assert argmax_agree(b2[s], ref, L, M), s
+
+
+def test_c4_fp64_stop_index(sp):
+    """The exact-tau stop (sparc_ldpc.py:204, amp_test.py:14-50) in binary64
+    at C4: the estimate after the reference's own stop index t_ref (t_ref
+    updates, the early stop off) matches the reference's returned estimate,
+    and this build's stop index lies within STOP_BOUND iterations of t_ref.
+    The index itself cannot be bit-pinned: tau repeats exactly only once the
+    iterates reach a fixed point to the last ulp, and the summation order of
+    Ab / sum(z^2) differs from NumPy's."""
+    STOP_BOUND = 3
+    g = golden("c4.npz")
+    L, M, n, T, NS = (int(g[k]) for k in ("L", "M", "n", "T", "NS"))
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp64")
+    Pl = float(g["P"]) / L * np.ones(L)
+    for k in (0, 1):
+        y = g[f"y_{k}"].reshape(1, -1)
+        t_ref = int(g[f"t_stop_{k}"])
+        # t_ref = T-1 is also what amp_test returns when its loop ran out (T
+        # updates, no stop): then the estimate after T updates is the match
+        cands = (t_ref, T) if t_ref == T - 1 else (t_ref,)
+        errs = []
+        for upd in cands:
+            b, _ = op.amp_batch(y, Pl, upd, early_stop=False)
+            errs.append((rel(b[0, :NS * M], g[f"beta_final_{k}"]),  # the fixture stores fp32
+                         abs(np.linalg.norm(b[0]) / float(g[f"beta_final_norm_{k}"]) - 1)))
+        assert any(e1 <= 1e-7 and e2 <= 1e-11 for e1, e2 in errs), (k, errs)
+        _, it = op.amp_batch(y, Pl, T)
+        # amp_test returns T-1 when the loop ran out (the reference's t after its loop)
+        t_ours = min(int(it[0]), T - 1)
+        assert abs(t_ours - t_ref) <= STOP_BOUND, (k, t_ours, t_ref)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_cached_operator_two_powers(sp, prec):
+    """One cached operator (sparc_transforms' _OP_CACHE) decoding at two total
+    powers P at the same (B, T): the replayed hipGraph must read the new P
+    (the Onsager term z/tau^2 (P - sum(beta^2)/n), sparc_ldpc.py:220)."""
+    L, M, T = 64, 64, 10
+    n = int(L * np.log2(M))
+    Ab, Az, _ = sp.sparc_transforms(L, M, n, precision=prec)
+    oAb, oAz, _ = orc.sparc_transforms(L, M, n)
+    outs = {}
+    for P in (2.0, 4.0, 2.0):
+        Pl = P / L * np.ones(L)
+        _, y = orc.rep_inputs(L, M, n, Pl, 0.7, oAb, 11)
+        b = sp.amp(y, 0, Pl, L, M, T, Ab, Az)
+        ref = orc.amp(y, 0, Pl, L, M, T, oAb, oAz)
+        assert rel(b, ref) <= TOL[prec], P
+        if P in outs:
+            assert np.array_equal(b, outs[P])
+        outs[P] = b

@@ -165,28 +165,49 @@ def _gloo_worker(rank, world, port, out):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import sparc_ldpc_amd as sp
     from sparc_ldpc_amd import dist
-    dist.init("gloo")
+    dist.init("socket")
+    assert dist.backend() == "socket"
     res = sp.ber_point(_fake_round, 4608, 7, 250, 4, rank, world, dist.allreduce_sum, seed_base=100)
     c = dist.allreduce_sum(np.array([rank + 1], dtype=np.int64))
-    out.put((rank, res, int(c[0])))
+    m = dist.allreduce_max(np.array([0.5 * rank, -rank], dtype=np.float64))
+    f = dist.allreduce_sum(np.array([0.1 * (rank + 1)] * 3, dtype=np.float64))
+    dist.barrier()
+    out.put((rank, res, int(c[0]), m.tolist(), f.tolist()))
     dist.finalize()
 
 
-def test_ber_point_two_ranks_gloo_equals_single():
+@pytest.mark.parametrize("world", [2, 3])
+def test_ber_point_ranks_socket_equals_single(world):
+    """The counter all-reduce over the dist module's TCP star (the CPU backend;
+    RCCL carries the same calls on GPUs): a sharded ber_point equals the
+    single-process one over the same seeds."""
     import multiprocessing as mp
     import sparc_ldpc_amd as sp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     got = [q.get(timeout=120) for _ in ps]
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    single = sp.ber_point(_fake_round, 4608, 7, 250, 8, seed_base=100)
-    for rank, res, csum in got:
-        assert csum == 3  # the counter all-reduce itself
+    single = sp.ber_point(_fake_round, 4608, 7, 250, 4 * world, seed_base=100)
+    for rank, res, csum, mx, fs in got:
+        assert csum == world * (world + 1) // 2  # the counter all-reduce itself
+        assert mx == [0.5 * (world - 1), 0.0]
+        assert fs == got[0][4]  # rank-order float sums: every rank gets the same bits
         assert res["blocks"] == single["blocks"] and res["block_errors"] == single["block_errors"]
         assert abs(res["BER"] - single["BER"]) <= 1e-15
+
+
+def test_allreduce_refuses_without_communicator(monkeypatch):
+    """WORLD_SIZE > 1 without dist.init(): never this rank's counts as the job's."""
+    from sparc_ldpc_amd import dist
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(dist, "_COMM", None)
+    with pytest.raises(dist.DistError):
+        dist.allreduce_sum(np.array([1], dtype=np.int64))
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert dist.allreduce_sum(np.array([5], dtype=np.int64)).tolist() == [5]

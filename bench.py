@@ -90,7 +90,7 @@ def _cpu_worker(args):
     Pl = P / L * np.ones(L)
     _, y = orc.rep_inputs(L, M, n, Pl, sigma, Ab, seed)
     t0 = time.time()
-    orc.amp(y, sigma, Pl, L, M, Tsample, Ab, Az)
+    orc._amp_core(y, Pl, L, M, Tsample, Ab, Az, None, early_stop=False)  # exactly Tsample iterations
     return t0, time.time()
 
 

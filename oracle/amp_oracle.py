@@ -163,13 +163,15 @@ def pa_parameterised(L, C, P, a, f):
     return pa
 
 
-def _amp_core(y, Pl, L, M, T, Ab, Az, beta):
+def _amp_core(y, Pl, L, M, T, Ab, Az, beta, early_stop=True):
     """The loop of sparc_ldpc.py:189-222 (== amp_test.py:14-50), returning (beta, t).
 
     ``beta`` is None for the zero start.  The reference's sentinel
     ``β.all()==None`` (sparc_ldpc.py:192) no longer recognises its own default
     under NumPy >= 2, so callers pass None explicitly here; the zero start is
     bit-identical to passing zeros because y - Ab(0) == y exactly.
+    ``early_stop=False`` (bench.py's CPU baseline only) skips the :204 test so
+    that exactly T iterations run, as in the GPU bench.
     """
     P = np.sum(Pl)
     n = y.size
@@ -183,7 +185,7 @@ def _amp_core(y, Pl, L, M, T, Ab, Az, beta):
     t = None
     for t in range(T):
         τ = np.sqrt(np.sum(z ** 2) / n)                      # :203
-        if τ == last_τ:                                       # :204 exact-equality stop
+        if early_stop and τ == last_τ:                        # :204 exact-equality stop
             return β, t
         last_τ = τ
         s = β + Az(z)                                         # :213

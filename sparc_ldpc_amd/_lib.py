@@ -38,7 +38,7 @@ EXPORTS = (
     "sa_reserve", "sa_stage", "sa_stage_power_batch", "sa_run", "sa_wait", "sa_fetch", "sa_fetch_z", "sa_run_event_ms",
     "sa_profile", "sa_profile_rep", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
-    "sa_threshold", "sa_cancel", "sa_plan",
+    "sa_threshold", "sa_cancel", "sa_plan", "sa_stage_onehot_scaled", "sa_cancel_scaled",
 )
 
 _P = ct.c_void_p
@@ -71,6 +71,8 @@ _SIG = {
     "sa_cancel": (_I, [_P, _I, ct.POINTER(ct.c_int32), _P]),
     "sa_plan": (_I, [_P, _I, ct.POINTER(ct.c_int64)]),
     "sa_stage_onehot": (_I, [_P, _I, ct.POINTER(ct.c_int32)]),
+    "sa_stage_onehot_scaled": (_I, [_P, _I, ct.POINTER(ct.c_int32), ct.c_double]),
+    "sa_cancel_scaled": (_I, [_P, _I, ct.POINTER(ct.c_int32), ct.c_double, _P]),
     "sa_llr": (_I, [_P, _I, _I, _I, _P, _I]),
     "sa_soft_beta0": (_I, [_P, _I, _I, _I, _P, _I]),
     "sa_hard_cancel": (_I, [_P, _I, _I, _I, _P, _I, _P, ct.POINTER(ct.c_int32)]),

@@ -122,37 +122,53 @@ def amp_ldpc_sim(sparcparams: SPARCParams, ldpcparams=None, a=None, f=None, C=No
     return ber_amp, None, None, R
 
 
-def mc_decode(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True):
-    """Batched Monte-Carlo reps on one device (SURVEY §8d synthetic inputs).
+def _draw_reps(seeds, L, M, n, sigma):
+    """Rep with seed s: ``RandomState(s)`` draws the L section indices uniform
+    in [0, M) (the law of random bits -> bits2indices) and then the noise
+    N(0, σ²) (n values) — SURVEY §8d's synthetic inputs."""
+    idx = np.empty((len(seeds), L), dtype=np.int32)
+    noise = np.empty((len(seeds), n))
+    for i, s in enumerate(seeds):
+        rs = np.random.RandomState(s)
+        idx[i] = rs.randint(0, M, L)
+        noise[i] = rs.randn(n)
+    noise *= sigma
+    return idx, noise
 
-    Rep with seed s: ``RandomState(s)`` draws the L section indices uniform
-    in [0, M) (the same law as random bits -> bits2indices) and then the
-    noise N(0, σ²) (n values).  Encoding x = A β₀, decoding and the section
-    decisions run on the device.  Returns per-rep int64 arrays
-    (bit_errors, iters) in seed order.
+
+def mc_decode(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True):
+    """Batched Monte-Carlo reps on one device (the rep body of sparc_ldpc.py:
+    423-462 on SURVEY §8d's synthetic inputs, ``_draw_reps``).
+
+    Encoding x = A β₀ + noise (sa_encode), the decode and the section
+    decisions run on the device; only the indices and the noise cross PCIe.
+    The host draws the next batch while the device decodes the current one
+    (the decode is asynchronous until the decisions are read).  Returns per-rep
+    int64 arrays (bit_errors, iters) in seed order.
     """
     L, M, n = op.L, op.M, op.n
     Pl = np.asarray(Pl, dtype=np.float64)
-    c = np.sqrt(n * Pl)
     seeds = list(seeds)
     bit_errors = np.zeros(len(seeds), dtype=np.int64)
     iters = np.zeros(len(seeds), dtype=np.int64)
-    for s0 in range(0, len(seeds), batch):
-        chunk = seeds[s0:s0 + batch]
+    if not seeds:
+        return bit_errors, iters
+    chunks = [seeds[i:i + batch] for i in range(0, len(seeds), batch)]
+    op.reserve(len(chunks[0]), T)
+    op.stage_power(len(chunks[0]), Pl)
+    nxt = _draw_reps(chunks[0], L, M, n, sigma)
+    s0 = 0
+    for k, chunk in enumerate(chunks):
+        idx, noise = nxt
         B = len(chunk)
-        idx = np.empty((B, L), dtype=np.int64)
-        noise = np.empty((B, n))
-        for i, s in enumerate(chunk):
-            rs = np.random.RandomState(s)
-            idx[i] = rs.randint(0, M, L)
-            noise[i] = rs.randn(n) * sigma
-        beta0 = np.zeros((B, L * M))
-        beta0[np.arange(B)[:, None], np.arange(L)[None, :] * M + idx] = c[None, :]
-        y = op.Ab_batch(beta0) + noise
-        _, it = op.amp_batch(y, Pl, T, None, early_stop)
+        op.encode(idx, noise)
+        op.run(B, T, early_stop=early_stop)
+        # host draws of the next batch overlap the device decode
+        nxt = _draw_reps(chunks[k + 1], L, M, n, sigma) if k + 1 < len(chunks) else None
         rx = op.decide(B).astype(np.int64)
-        bit_errors[s0:s0 + B] = _popcount(np.bitwise_xor(idx, rx)).sum(axis=1)
-        iters[s0:s0 + B] = it
+        bit_errors[s0:s0 + B] = _popcount(np.bitwise_xor(idx.astype(np.int64), rx)).sum(axis=1)
+        iters[s0:s0 + B] = op.iters(B)
+        s0 += B
     return bit_errors, iters
 
 
@@ -248,37 +264,85 @@ def waterfall_plain(L, M, P, R, T, ebno_dbs, min_errors=200, max_blocks=250, csv
 
 
 def amp_test_reps(L=512, M=512, L_zero=154, P=4, snr_dB=10, r_sparc=1, T=64, repeats=100,
-                  backend=None, precision=None):
-    """The reps loop of amp_test.py:161-253: per rep, hard-init AMP on the
-    first L_zero sections (shortened operator), soft-init AMP with the 0/1
-    β₀, and zero-init AMP; returns the three mean BERs.  Draws come from
-    np.random in the reference's order (:185-200)."""
+                  backend=None, precision=None, batch=64, rank=0, world=1, allreduce=None, return_counts=False):
+    """The reps loop of amp_test.py:161-253, batched on the device and sharded
+    over ranks.  Per rep the reference draws the message bits and the noise
+    (:185-199), then decodes three times and adds each decode's BER:
+
+      * hard init (:201-221): the sections from L_zero on are taken as decoded
+        with the 0/1 start beta_0 = beta / sqrt(n P / L) (its first L_zero
+        sections zeroed); y' = y - Ab(beta_0) is decoded by AMP on the
+        shortened operator over the first L_zero sections
+        (sparc_transforms_shorter), BER over those sections;
+      * soft init (:223-232): AMP over all L sections from beta_0;
+      * no init (:234-241): AMP from zero.
+
+    Every rank draws every rep from np.random in the reference's order (so a
+    seeded call reproduces the reference's reps, whatever the world size) and
+    decodes the reps i with i % world == rank, ``batch`` at a time: encode,
+    cancellation, the three decodes and the decisions all on the device,
+    sharing one full and one shortened operator.  The per-rep bit-error counts
+    are summed over ranks (``allreduce``, dist.allreduce_sum) and the BERs
+    accumulated in rep order as the reference does (ber += errors / total_bits).
+    Returns (ber_hard, ber_soft, ber_no_init), plus the (repeats, 3) int64
+    error counts with ``return_counts``.
+    """
     snr = 10 ** (snr_dB / 20)
     sigma = np.sqrt(P / snr)
     Pl = P / L * np.ones(L)
     logm = np.log2(M)
     total_bits = int(L * logm)
     n = int(L * np.log2(M) / r_sparc)
-    ber_hard = ber_soft = ber_no_init = 0.0
-    for _ in range(repeats):
-        bits = np.random.randint(0, 2, total_bits).tolist()
-        idx = np.asarray(bits2indices(bits, M))
-        Ab, Az, ordering = sparc_transforms(L, M, n, backend=backend, precision=precision)
-        beta = np.zeros((L * M, 1))
-        beta[np.arange(L) * M + idx, 0] = np.sqrt(n * Pl)
-        x = Ab(beta)
-        y = (x + np.random.randn(n, 1) * sigma).reshape(-1, 1)
-        beta_0 = beta / np.sqrt(n * P / L)
-        beta_0[:L_zero * M] = 0
-        y_new = y - Ab(beta_0)
-        Ab_n, Az_n = sparc_transforms_shorter(L_zero, M, n, ordering, backend=backend, precision=precision)
-        bh = amp(y_new, sigma, Pl[:L_zero], L_zero, M, T, Ab_n, Az_n).reshape(-1)
-        ber_hard += ber_of(idx[:L_zero], bh.reshape(L_zero, M).argmax(1), total_bits)
-        bs = amp(y, sigma, Pl, L, M, T, Ab, Az, beta_0).reshape(-1)
-        ber_soft += ber_of(idx, bs.reshape(L, M).argmax(1), total_bits)
-        bz = amp(y, sigma, Pl, L, M, T, Ab, Az).reshape(-1)
-        ber_no_init += ber_of(idx, bz.reshape(L, M).argmax(1), total_bits)
-    return ber_hard / repeats, ber_soft / repeats, ber_no_init / repeats
+    mine = [i for i in range(repeats) if i % world == rank]
+    idx = np.empty((len(mine), L), dtype=np.int32)
+    noise = np.empty((len(mine), n))
+    w = 1 << np.arange(int(logm) - 1, -1, -1, dtype=np.int64)
+    k = 0
+    for i in range(repeats):
+        bits = np.random.randint(0, 2, total_bits)          # :185
+        z = np.random.randn(n, 1) * sigma                   # :198
+        if i % world == rank:
+            idx[k] = (bits.reshape(L, -1).astype(np.int64) * w).sum(axis=1)  # bits2indices, :187
+            noise[k] = z.reshape(-1)
+            k += 1
+    ordering = make_ordering(L, M, n, 0)
+    op = SparcOperator(L, M, n, ordering, backend, precision)
+    op_h = SparcOperator(L_zero, M, n, ordering[:L_zero], backend, precision)
+    scale = 1.0 / np.sqrt(n * P / L)                         # beta_0 = beta / sqrt(n P / L), :202
+    counts = np.zeros((repeats, 3), dtype=np.int64)
+    for s0 in range(0, len(mine), batch):
+        ib = idx[s0:s0 + batch]
+        B = ib.shape[0]
+        op.reserve(B, T)
+        op_h.reserve(B, T)
+        op.stage_power(B, Pl)
+        op_h.stage_power(B, Pl[:L_zero])
+        op.encode(ib, noise[s0:s0 + B])                      # y = Ab(beta) + z, :193-199
+        ib0 = ib.copy()
+        ib0[:, :L_zero] = -1                                 # beta_0[:L_zero*M] = 0, :204
+        op.cancel(ib0, op_h, scale)                          # y_new = y - Ab(beta_0), :208-210
+        op_h.run(B, T)
+        rx_h = op_h.decide(B).astype(np.int64)
+        op.stage_onehot(ib0, scale)
+        op.run(B, T, beta0=True)                             # soft init, :225
+        rx_s = op.decide(B).astype(np.int64)
+        op.run(B, T)                                         # no init, :235
+        rx_z = op.decide(B).astype(np.int64)
+        reps = mine[s0:s0 + B]
+        ib64 = ib.astype(np.int64)
+        counts[reps, 0] = _popcount(np.bitwise_xor(ib64[:, :L_zero], rx_h)).sum(axis=1)
+        counts[reps, 1] = _popcount(np.bitwise_xor(ib64, rx_s)).sum(axis=1)
+        counts[reps, 2] = _popcount(np.bitwise_xor(ib64, rx_z)).sum(axis=1)
+    if world > 1:
+        if allreduce is None:
+            raise ValueError("amp_test_reps: world > 1 needs allreduce (dist.allreduce_sum)")
+        counts = allreduce(counts)
+    ber = [0.0, 0.0, 0.0]
+    for i in range(repeats):                                 # the reference's float accumulation
+        for j in range(3):
+            ber[j] = ber[j] + int(counts[i, j]) / total_bits
+    out = (ber[0] / repeats, ber[1] / repeats, ber[2] / repeats)
+    return (out, counts) if return_counts else out
 
 
 def amp_init_test(L, M, snr_dB, P, r_sparc, backend=None, precision=None):

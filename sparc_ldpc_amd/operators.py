@@ -215,6 +215,12 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, dptr(out), iters.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return out, iters
 
+    def iters(self, B):
+        """Stop index of each codeword of the last decode (T when the loop ran out)."""
+        it = np.empty(B, dtype=np.int32)
+        check(self._lib.sa_fetch(self._ctx, B, None, it.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
+        return it
+
     SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43")
 
     def fetch_z(self, B):
@@ -274,11 +280,15 @@ class SparcOperator:
         check(self._lib.sa_encode(self._ctx, B, idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32)), nz))
         return B
 
-    def stage_onehot(self, idx):
-        """Stage the one-hot β₀ of section indices idx (B, L) for run(..., beta0=True)."""
+    def stage_onehot(self, idx, scale=None):
+        """Stage the one-hot β₀ of section indices idx (B, L) for run(..., beta0=True):
+        c_l at idx[b, l]; with ``scale``, scale * c_l and idx -1 = an all-zero section."""
         idx = np.ascontiguousarray(idx, dtype=np.int32)
-        check(self._lib.sa_stage_onehot(self._ctx, idx.shape[0],
-                                        idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
+        p = idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))
+        if scale is None:
+            check(self._lib.sa_stage_onehot(self._ctx, idx.shape[0], p))
+        else:
+            check(self._lib.sa_stage_onehot_scaled(self._ctx, idx.shape[0], p, float(scale)))
 
     def llr(self, B, l0, ns, out=None):
         """LDPC-bit LLRs of sections [l0, l0+ns) of the current β (sparc_ldpc.py:470-479).
@@ -319,12 +329,16 @@ class SparcOperator:
                                      idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
         return idx
 
-    def cancel(self, idx, dst):
-        """Stage y - A β(idx) (idx (B, L), -1 = keep) as dst's input y."""
+    def cancel(self, idx, dst, scale=None):
+        """Stage y - A β(idx) (idx (B, L), -1 = keep) as dst's input y; β(idx) has
+        c_l at idx[b, l], or scale * c_l with ``scale``."""
         idx = np.ascontiguousarray(idx, dtype=np.int32)
         assert idx.ndim == 2 and idx.shape[1] == self.L
-        check(self._lib.sa_cancel(self._ctx, idx.shape[0], idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32)),
-                                  dst.ctx))
+        p = idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))
+        if scale is None:
+            check(self._lib.sa_cancel(self._ctx, idx.shape[0], p, dst.ctx))
+        else:
+            check(self._lib.sa_cancel_scaled(self._ctx, idx.shape[0], p, float(scale), dst.ctx))
 
     def subset(self, sections) -> "SparcOperator":
         """Operator over the given parent sections (sparc_transforms_shorter)."""

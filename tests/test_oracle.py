@@ -180,3 +180,33 @@ def test_c4_oracle_matches_reference():
     assert np.array_equal(b[:NS * M].astype(np.float32), g["beta_final_1"])
     assert np.array_equal(orc.section_argmax(b, L, M), g["argmax_final_1"])
     assert float(np.linalg.norm(b)) == float(g["beta_final_norm_1"])
+
+
+def test_oracle_amp_test_reps_golden():
+    """The oracle reproduces the reference's seeded amp_test.py reps (first 3 of
+    the small case of tests/golden/amp_test_reps.npz): hard / soft / no-init
+    error counts, with the draws of amp_test.py:185-199."""
+    import json
+    with open(os.path.join(GOLDEN, "amp_test_reps.json")) as fh:
+        m = json.load(fh)["small"]
+    g = golden("amp_test_reps.npz")
+    L, M, Lz, P, T = m["L"], m["M"], m["L_zero"], m["P"], m["T"]
+    n, sigma = m["n"], m["sigma"]
+    tb = int(L * np.log2(M))
+    Pl = P / L * np.ones(L)
+    Ab, Az, ordering = orc.sparc_transforms(L, M, n)
+    Ab_n, Az_n = orc.sparc_transforms_shorter(Lz, M, n, ordering)
+    np.random.seed(m["seed"])
+    for r in range(3):
+        idx = np.asarray(orc.bits2indices(np.random.randint(0, 2, tb).tolist(), M))
+        noise = np.random.randn(n, 1) * sigma
+        beta = np.zeros((L * M, 1)); beta[np.arange(L) * M + idx, 0] = np.sqrt(n * Pl)
+        y = Ab(beta) + noise
+        b0 = beta / np.sqrt(n * P / L); b0[:Lz * M] = 0
+        bh = orc.amp(y - Ab(b0), sigma, Pl[:Lz], Lz, M, T, Ab_n, Az_n)
+        bs = orc.amp(y, sigma, Pl, L, M, T, Ab, Az, b0)
+        bz = orc.amp(y, sigma, Pl, L, M, T, Ab, Az)
+        got = [round(orc.ber_indices(idx[:Lz], orc.section_argmax(bh, Lz, M), 1)),
+               round(orc.ber_indices(idx, orc.section_argmax(bs, L, M), 1)),
+               round(orc.ber_indices(idx, orc.section_argmax(bz, L, M), 1))]
+        assert got == g["small_counts"][r].tolist(), (r, got)

@@ -28,6 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+I8_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF bf16 rate per clock (MI355X_MICROARCH.md, Matrix cores)
+NP_Z, NP_B = 3, 4      # int8 digit planes of z and beta on the dense GEMM path (csrc/dense_i8.hip)
 PROFILE_REP = 16       # back-to-back launches per event pair (roofline timing)
 
 WORKLOADS = {
@@ -78,6 +80,14 @@ def row_bytes(n, B, G, s):
 def gemv_bytes(L, M, n):
     """4·n·L·M + 4·(n + L·M) per fp32 GEMV."""
     return 4 * n * L * M + 4 * (n + L * M)
+
+
+def i8_gemm_ops(L, M, n, B, planes):
+    """Algorithmic int8 multiply-adds x 2 of one dense GEMM on the matrix cores:
+    `planes` digit planes of B codewords against the n x L·M ±1 matrix (the
+    fp32-equivalent GEMM of SURVEY §8d is 2·n·L·M·B flops: this counts each
+    digit plane's product, the work the int8 MFMA actually does)."""
+    return 2 * planes * B * n * L * M
 
 
 def _cpu_worker(args):
@@ -251,21 +261,30 @@ def main():
             "k_sec": sec_bytes(L, M, n, wv, B, G, s, plan["section_kernel"]),
             "k_row": row_bytes(n, B, G, s),
         }
+    elif plan["section_kernel"] == "dense_mfma":
+        per = {"k_dense_az": i8_gemm_ops(L, M, n, B, NP_Z), "k_dense_ab": i8_gemm_ops(L, M, n, B, NP_B)}
     else:
         per = {"k_dense_az": gemv_bytes(L, M, n) * B, "k_dense_ab": gemv_bytes(L, M, n) * B,
                "k_dense_den": B * (8 * 4 * L * M + 8 * L * M), "k_row": row_bytes(n, B, 8, s)}
     share = {k: kinds[k][0] * kinds[k][1] for k in per}
     dom = max(share, key=share.get)
     dom_ms = kinds_rep[dom][0]
-    achieved = per[dom] / (dom_ms * 1e-3) / 1e9
+    mfma = plan["section_kernel"] == "dense_mfma"
+    achieved = per[dom] / (dom_ms * 1e-3) / (1e12 if mfma else 1e9)
+    peak = I8_PEAK_TOPS if mfma else HBM_PEAK_GBS
     pmc = load_pmc(f"{args.workload}_{args.backend}_{args.precision}_B{B}",
                    {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom))
     kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom)
+    if mfma:
+        kname = "k_gemm_i8 (" + {"k_dense_az": f"A^T z, {NP_Z} digit planes",
+                                 "k_dense_ab": f"A beta, {NP_B} digit planes"}[dom] + ")"
     roofline = {
-        "bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "bound": "mfma" if mfma else "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": peak,
+        "unit": "TFLOP/s" if mfma else "GB/s", "frac": round(achieved / peak, 4),
         "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-        "algorithmic_bytes_per_launch": per[dom], "avg_launch_ms": round(dom_ms, 5),
+        ("algorithmic_int8_ops_per_launch" if mfma else "algorithmic_bytes_per_launch"): per[dom],
+        **({"ops": "int8 multiply-adds x 2 (TOP/s)"} if mfma else {}),
+        "avg_launch_ms": round(dom_ms, 5),
         "kernel_ms": {k: round(v[0], 5) for k, v in kinds_rep.items() if v[1]},
         "kernel_ms_event_bracketed": {k: round(v[0], 5) for k, v in kinds.items() if v[1]},
         "timing": f"HIP events on the library stream around {PROFILE_REP} back-to-back launches per kernel",

@@ -39,7 +39,9 @@ enum {
 
 enum {
   SA_BACKEND_HADAMARD = 0,  /* matrix-free sub-sampled Walsh-Hadamard operator (default) */
-  SA_BACKEND_DENSE = 1      /* materialised n x (L*M) fp32 design matrix, GEMV-streamed */
+  SA_BACKEND_DENSE = 1      /* materialised n x (L*M) design matrix: fp32 GEMVs for B < 4
+                               codewords, int8 matrix-core GEMMs on exact +-1 entries with
+                               three-digit fixed-point vectors for B >= 4 */
 };
 
 enum { SA_PREC_F32 = 0, SA_PREC_F64 = 1 };
@@ -110,10 +112,12 @@ int sa_fetch_z(sa_ctx* ctx, int B, double* z_out);
 double sa_run_event_ms(sa_ctx* ctx);
 
 /* Per-kernel device time of one EAGER decode of the staged batch (every
- * launch bracketed by HIP events on the context's stream).  out[11]:
+ * launch bracketed by HIP events on the context's stream).  out[13]:
  * {mean ms, launches} for kernel kinds 0 section (k_sec), 1 row (k_row),
- * 2 dense A^T z GEMV, 3 dense denoiser, 4 dense A beta GEMV; out[10] = total
- * ms of the sequence.  Leaves the decode's results in place like sa_run. */
+ * 2 dense A^T z (fp32 GEMV; int8 MFMA GEMM for B >= 4), 3 dense denoiser,
+ * 4 dense A beta (GEMV; int8 MFMA GEMM for B >= 4), 5 int8 digit-plane
+ * quantisation of z / beta0; out[12] = total ms of the sequence.  Leaves the
+ * decode's results in place like sa_run. */
 int sa_profile(sa_ctx* ctx, int B, int T, int flags, double* out);
 /* The same with every bracketed launch issued `rep` (1..1024) times back to
  * back between its events: mean = elapsed / rep, i.e. the launch's duration
@@ -183,7 +187,8 @@ int sa_cancel_scaled(sa_ctx* ctx, int B, const int32_t* idx, double scale, sa_ct
 
 /* Introspection. */
 /* The kernels a decode of B codewords runs: out8 = {section kernel (0 k_sec,
- * 1 k_sec2, 2 k_secb, 3 dense GEMVs), Ab partials per codeword, row splits,
+ * 1 k_sec2, 2 k_secb, 3 dense fp32 GEMVs, 4 k_sec4, 5 k_sec43, 6 dense int8
+ * MFMA GEMMs), Ab partials per codeword, row splits,
  * codewords per batched workgroup, z^2 partials, w, row kernel (1 k_row2,
  * 0 k_row), 0}. */
 int sa_plan(sa_ctx* ctx, int B, int64_t* out8);

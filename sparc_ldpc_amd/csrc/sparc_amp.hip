@@ -1921,11 +1921,18 @@ __global__ void __launch_bounds__(256) k_dense_ab(DenseArgs a, const float* tau)
   }
 }
 
+#include "dense_i8.hip"
+
 // Dense-path denoiser: sums the RS Az partials of one section (wave) and
 // applies denoise_section; writes tau (workgroup 0) and beta^2 partials.
+// On the int8 matrix-core path (bq != NULL) it also writes the new beta's
+// kI8NPB base-256 digit planes at the fixed scale bfix[0] (beta_l <= c_l, so
+// one power-of-two scale per decode: dense_i8.hip).
 template <int E>
 __global__ void __launch_bounds__(256) k_dense_den(DenseArgs a, const float* c, float* beta,
-                                                   float* bbp, float* tau_out, int* iters, int G) {
+                                                   float* bbp, float* tau_out, int* iters, int G,
+                                                   int8_t* bq, long long bq_ps, long long bq_ld,
+                                                   const double* bfix) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = blockIdx.x, b = blockIdx.y;
   const int l = g * 4 + wv;
@@ -1954,6 +1961,20 @@ __global__ void __launch_bounds__(256) k_dense_den(DenseArgs a, const float* c, 
     float bprev[E];
     load_section<float, E>(bl, bprev, lane, M);
     bb = denoise_section<float, E>(v, bprev, bl, lane, M, c[l], tau * tau, 1.0f);
+    if (bq) {
+      const double sf = bfix[0];
+      int8_t* qb = bq + (long long)b * bq_ld + (long long)l * M;
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        const int e = elem_index<E>(lane, i);
+        if (e < M) {
+          int d[kI8NPB];
+          i8_digits<kI8NPB>((int)rint((double)v[i] * sf), d);
+#pragma unroll
+          for (int p = 0; p < kI8NPB; ++p) qb[p * bq_ps + e] = (int8_t)d[p];
+        }
+      }
+    }
   }
   if (lane == 0) bbw[wv] = bb;
   __syncthreads();
@@ -1999,7 +2020,7 @@ struct Prof {
   }
 };
 
-enum { K_SEC = 0, K_ROW = 1, K_DAZ = 2, K_DDEN = 3, K_DAB = 4, K_NKINDS = 5 };
+enum { K_SEC = 0, K_ROW = 1, K_DAZ = 2, K_DDEN = 3, K_DAB = 4, K_QNT = 5, K_NKINDS = 6 };
 
 #define PROF_REPS(c) for (int _rep = 0, _nrep = (c)->prof ? (c)->prof->rep : 1; _rep < _nrep; ++_rep)
 
@@ -2030,6 +2051,13 @@ struct sa_ctx {
   uint16_t* d_fwd = nullptr;
   uint32_t* d_fwd2 = nullptr;
   float* d_A = nullptr;
+  // int8 matrix-core dense path (B >= 4; dense_i8.hip): A8 [np8][LMp8], AT8 [LMp8][np8],
+  // digit planes of z [3][Bp8][np8] and beta [3][Bp8][LMp8], per-codeword scales
+  int8_t *d_A8 = nullptr, *d_AT8 = nullptr, *d_zq = nullptr, *d_bq = nullptr;
+  double *d_zsc = nullptr, *d_bsc0 = nullptr, *d_bfix = nullptr;
+  long long np8 = 0, LMp8 = 0;
+  int Bp8 = 0;
+  double cmax = 0;  // max_l sqrt(n Pl_l) of the shared power allocation
   // workspace
   int Bcap = 0, Tcap = 0;
   void *d_y = nullptr, *d_z = nullptr, *d_beta = nullptr, *d_out = nullptr, *d_abp = nullptr;
@@ -2096,7 +2124,93 @@ void free_workspace(sa_ctx* c) {
   }
 }
 
+// ---- int8 matrix-core dense path (dense_i8.hip) -------------------------
+constexpr int kI8MinB = 4;    // batches at least this large take the GEMM path
+constexpr int kI8MaxS = 16;   // K splits of the A beta GEMM (its Ab partials)
+
+bool use_i8(const sa_ctx* c, int B) {
+  return c->backend == SA_BACKEND_DENSE && B >= kI8MinB && !getenv("SPARC_AMP_NO_I8");
+}
+
+int i8_bp(int B) { return (B + kI8TX - 1) / kI8TX * kI8TX; }
+
+// K splits of the A beta GEMM for B codewords: the fewest (workgroup rounds x
+// stages per workgroup), i.e. the shortest critical path on n_cus CUs
+int i8_splits(const sa_ctx* c, int B) {
+  const long long tiles = (long long)(c->np8 / kI8TY) * (i8_bp(B) / kI8TX);
+  const int nst = (int)(c->LMp8 / kI8KS);
+  int best = 1;
+  long long bcost = -1;
+  for (int S = 1; S <= kI8MaxS; ++S) {
+    const long long rounds = (tiles * S + c->n_cus - 1) / c->n_cus;
+    const long long cost = rounds * ((nst + S - 1) / S);
+    if (bcost < 0 || cost < bcost) { bcost = cost; best = S; }
+  }
+  return best;
+}
+
+// The fixed digit scale of beta on the GEMM path: beta_l <= c_l (the softmax
+// weights sum to one), so s = 2^(30 - E) with c_max (1 + 2^-10) < 2^E keeps
+// |rint(beta s)| <= 2^30 (four digits); bfix = {s, 1 / (s sqrt(n))} in device
+// memory (a replayed graph reads the current value).
+int i8_set_bfix(sa_ctx* c) {
+  int E = 0;
+  if (c->cmax > 0) (void)std::frexp(c->cmax * (1.0 + 1.0 / 1024), &E);
+  const double sfix = std::ldexp(1.0, i8_bits<kI8NPB>() - E);
+  const double h[2] = {sfix, 1.0 / (sfix * std::sqrt((double)c->n))};
+  HIP_TRY(hipMemcpyAsync(c->d_bfix, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+// Builds A8 / AT8 on first use and sizes the digit planes for B codewords.
+int ensure_i8(sa_ctx* c, int B) {
+  if (!use_i8(c, B)) return SA_OK;
+  int rc;
+  if (!c->d_A8) {
+    c->np8 = ((long long)c->n + kI8TY - 1) / kI8TY * kI8TY;
+    c->LMp8 = ((long long)c->L * c->M + kI8TY - 1) / kI8TY * kI8TY;
+    const size_t bytes = (size_t)c->np8 * (size_t)c->LMp8;
+    if ((rc = dev_alloc(c, (void**)&c->d_A8, bytes))) return rc;
+    if ((rc = dev_alloc(c, (void**)&c->d_AT8, bytes))) return rc;
+    if ((rc = dev_alloc(c, (void**)&c->d_bfix, 2 * sizeof(double)))) return rc;
+    uint32_t* d_ord = nullptr;
+    HIP_TRY(hipMalloc(&d_ord, c->ordering.size() * 4));
+    HIP_TRY(hipMemcpyAsync(d_ord, c->ordering.data(), c->ordering.size() * 4, hipMemcpyHostToDevice, c->stream));
+    k_i8_build<<<8192, 256, 0, c->stream>>>(d_ord, c->d_A8, c->L, c->M, c->n, c->w, c->np8, c->LMp8, 0);
+    k_i8_build<<<8192, 256, 0, c->stream>>>(d_ord, c->d_AT8, c->L, c->M, c->n, c->w, c->LMp8, c->np8, 1);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_ord);
+    if (e != hipSuccess) return fail(SA_ERR_HIP, std::string("k_i8_build: ") + hipGetErrorString(e));
+    if (c->power_set && (rc = i8_set_bfix(c))) return rc;
+  }
+  const int Bp = i8_bp(B);
+  if (Bp > c->Bp8) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    drop_graphs(c);
+    dev_free(c->d_zq); dev_free(c->d_bq); dev_free(c->d_zsc); dev_free(c->d_bsc0);
+    c->d_zq = c->d_bq = nullptr;
+    c->d_zsc = c->d_bsc0 = nullptr;
+    c->Bp8 = 0;
+    const size_t zb = kI8NPZ * (size_t)Bp * (size_t)c->np8, bb = kI8NPB * (size_t)Bp * (size_t)c->LMp8;
+    if ((rc = dev_alloc(c, (void**)&c->d_zq, zb))) return rc;
+    if ((rc = dev_alloc(c, (void**)&c->d_bq, bb))) return rc;
+    if ((rc = dev_alloc(c, (void**)&c->d_zsc, (size_t)Bp * sizeof(double)))) return rc;
+    if ((rc = dev_alloc(c, (void**)&c->d_bsc0, (size_t)Bp * sizeof(double)))) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_zq, 0, zb, c->stream));  // K and codeword padding stays zero
+    HIP_TRY(hipMemsetAsync(c->d_bq, 0, bb, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->Bp8 = Bp;
+  }
+  return SA_OK;
+}
+
 int ensure_workspace(sa_ctx* c, int B, int T) {
+  if (c->backend == SA_BACKEND_DENSE) {
+    int rc8 = ensure_i8(c, B > c->Bcap ? B : c->Bcap);
+    if (rc8) return rc8;
+  }
   if (B <= c->Bcap && T <= c->Tcap) return SA_OK;
   HIP_TRY(hipStreamSynchronize(c->stream));
   drop_graphs(c);
@@ -2105,6 +2219,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   free_workspace(c);
   const size_t s = rsz(c), LM = (size_t)c->L * c->M;
   int Gmax = c->G > c->KS ? c->G : c->KS;
+  if (c->backend == SA_BACKEND_DENSE && Gmax < kI8MaxS) Gmax = kI8MaxS;
   if (c->Gb > Gmax) Gmax = c->Gb;
   if (c->G2 > Gmax) Gmax = c->G2;
   if (c->G3 > Gmax) Gmax = c->G3;
@@ -2395,28 +2510,85 @@ int launch_dense_ab(sa_ctx* c, int B, int t, int es, int mode) {
 }
 
 template <int E>
-void launch_dense_den_e(sa_ctx* c, int B, const DenseArgs& a) {
+void launch_dense_den_e(sa_ctx* c, int B, const DenseArgs& a, bool i8) {
   dim3 grid(c->Gd, B);
   if (c->prof) c->prof->begin(c->stream, K_DDEN);
   PROF_REPS(c) k_dense_den<E><<<grid, 256, 0, c->stream>>>(a, (const float*)c->d_c, (float*)c->d_beta,
-                                               (float*)c->d_bbp, (float*)c->d_tau, c->d_iters, c->Gd);
+                                               (float*)c->d_bbp, (float*)c->d_tau, c->d_iters, c->Gd,
+                                               i8 ? c->d_bq : nullptr, (long long)c->Bp8 * c->LMp8,
+                                               c->LMp8, c->d_bfix);
   if (c->prof) c->prof->end(c->stream);
 }
 
-int launch_dense_den(sa_ctx* c, int B, int t, int es) {
+// i8 = true: the Az of the matrix-core GEMM (one partial, d_azp[b][0][:]) and
+// the beta digit planes written for the next A beta GEMM
+int launch_dense_den(sa_ctx* c, int B, int t, int es, bool i8 = false) {
   DenseArgs a = dense_args(c, t, es, 0);
+  if (i8) a.RS = 1;
   switch (c->E) {
-    case 1: launch_dense_den_e<1>(c, B, a); break;
-    case 2: launch_dense_den_e<2>(c, B, a); break;
-    case 4: launch_dense_den_e<4>(c, B, a); break;
-    case 8: launch_dense_den_e<8>(c, B, a); break;
-    case 16: launch_dense_den_e<16>(c, B, a); break;
-    case 32: launch_dense_den_e<32>(c, B, a); break;
-    case 64: launch_dense_den_e<64>(c, B, a); break;
+    case 1: launch_dense_den_e<1>(c, B, a, i8); break;
+    case 2: launch_dense_den_e<2>(c, B, a, i8); break;
+    case 4: launch_dense_den_e<4>(c, B, a, i8); break;
+    case 8: launch_dense_den_e<8>(c, B, a, i8); break;
+    case 16: launch_dense_den_e<16>(c, B, a, i8); break;
+    case 32: launch_dense_den_e<32>(c, B, a, i8); break;
+    case 64: launch_dense_den_e<64>(c, B, a, i8); break;
     default: return fail(SA_ERR_UNSUPPORTED, "bad E");
   }
   HIP_TRY(hipGetLastError());
   return SA_OK;
+}
+
+// Digit planes of B vectors of length len (rows ld apart) -> q planes of K
+// bytes per row (K = np8 for z, LMp8 for beta), scales sc[b] = 1/(s_b sqrt(n)).
+template <int NP>
+int launch_i8_quant(sa_ctx* c, int B, const void* src, long long ld, int len, int8_t* q, long long K, double* sc) {
+  if (c->prof) c->prof->begin(c->stream, K_QNT);
+  PROF_REPS(c) k_i8_quant<NP><<<B, 256, 0, c->stream>>>((const float*)src, ld, len, q, (long long)c->Bp8 * K, K,
+                                                         sc, 1.0 / std::sqrt((double)c->n));
+  if (c->prof) c->prof->end(c->stream);
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
+// out[b][s][y] = (A v_b)_y restricted to K split s: the digit planes X
+// ([NP][Bp8][K]) against the +-1 matrix Y (rows of K bytes), Ny valid rows.
+template <int NP>
+int launch_gemm_i8(sa_ctx* c, int B, const int8_t* X, long long K, const int8_t* Y, long long Yrows, int Ny,
+                   float* out, long long ldb, long long lds, int S, const double* scale, int sst, int kind) {
+  I8Args a;
+  a.X = X; a.Y = Y; a.out = out; a.scale = scale;
+  a.xps = (long long)c->Bp8 * K; a.K = K; a.ldb = ldb; a.lds = lds;
+  a.nst = (int)(K / kI8KS);
+  a.kps = (a.nst + S - 1) / S;
+  a.XT = i8_bp(B) / kI8TX; a.YT = (int)(Yrows / kI8TY); a.S = S;
+  a.B = B; a.Ny = Ny; a.sst = sst;
+  if (i8_bp(B) > c->Bp8 || K % kI8KS || Yrows % kI8TY) return fail(SA_ERR_ARG, "k_gemm_i8: operand shapes");
+  const long long grid = (long long)a.XT * a.YT * S;
+  if (grid > 0x7fffffff) return fail(SA_ERR_UNSUPPORTED, "k_gemm_i8: grid too large");
+  if (c->prof) c->prof->begin(c->stream, kind);
+  PROF_REPS(c) k_gemm_i8<NP><<<(unsigned)grid, 512, I8Tile<NP>::Lds, c->stream>>>(a);
+  if (c->prof) c->prof->end(c->stream);
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
+// Ab of the beta staged in d_beta on the GEMM path: S Ab partials in d_abp
+// (quantised at a per-codeword scale: an arbitrary beta, e.g. beta0)
+int i8_ab_any(sa_ctx* c, int B, int S) {
+  const long long LM = (long long)c->L * c->M;
+  int rc = launch_i8_quant<kI8NPB>(c, B, c->d_beta, LM, (int)LM, c->d_bq, c->LMp8, c->d_bsc0);
+  if (rc) return rc;
+  return launch_gemm_i8<kI8NPB>(c, B, c->d_bq, c->LMp8, c->d_A8, c->np8, c->n, (float*)c->d_abp, (long long)S * c->n,
+                        c->n, S, c->d_bsc0, 1, K_DAB);
+}
+
+// Az of the z in d_z on the GEMM path into out[b][0 .. L*M) (rows ldb apart)
+int i8_az(sa_ctx* c, int B, float* out, long long ldb) {
+  int rc = launch_i8_quant<kI8NPZ>(c, B, c->d_z, c->n, c->n, c->d_zq, c->np8, c->d_zsc);
+  if (rc) return rc;
+  return launch_gemm_i8<kI8NPZ>(c, B, c->d_zq, c->np8, c->d_AT8, c->LMp8, c->L * c->M, out, ldb, 0, 1, c->d_zsc, 1,
+                        K_DAZ);
 }
 
 // ---- composite sequences (all asynchronous on c->stream) ----------------
@@ -2425,6 +2597,11 @@ int launch_dense_den(sa_ctx* c, int B, int t, int es) {
 template <typename real>
 int seq_ab(sa_ctx* c, int B) {
   int rc;
+  if (use_i8(c, B)) {
+    const int S = i8_splits(c, B);
+    if ((rc = i8_ab_any(c, B, S))) return rc;
+    return launch_row<real>(c, B, ROW_ABOUT, 0, 0, S, c->Gd);
+  }
   if (c->backend == SA_BACKEND_DENSE) {
     if ((rc = launch_dense_ab(c, B, 0, 0, 1))) return rc;
     return launch_row<real>(c, B, ROW_ABOUT, 0, 0, c->KS, c->Gd);
@@ -2439,6 +2616,7 @@ int seq_az(sa_ctx* c, int B);
 
 template <>
 int seq_az<float>(sa_ctx* c, int B) {
+  if (use_i8(c, B)) return i8_az(c, B, (float*)c->d_out, (long long)c->L * c->M);
   if (c->backend == SA_BACKEND_DENSE) {
     int rc = launch_dense_az(c, B, 0, 0, 1);
     if (rc) return rc;
@@ -2459,16 +2637,21 @@ template <typename real>
 int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const int es = (flags & SA_FLAG_NO_EARLY_STOP) ? 0 : 1;
   const bool dense = c->backend == SA_BACKEND_DENSE;
+  const bool i8 = use_i8(c, B);
+  const int S8 = i8 ? i8_splits(c, B) : 0;
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
   c->nz_cur = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;  // z^2 partials: k_row2 or k_row blocks
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
-  const int G = dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
+  const int G = i8 ? S8 : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
   int rc;
   k_fill32<<<(B + 255) / 256, 256, 0, c->stream>>>((uint32_t*)c->d_iters, 0xffffffffu, (size_t)B);
   if (has_b0) {
-    if (dense) {
+    if (i8) {
+      if ((rc = i8_ab_any(c, B, S8))) return rc;
+      if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, S8, c->Gd))) return rc;
+    } else if (dense) {
       if ((rc = launch_dense_ab(c, B, 0, 0, 1))) return rc;
       if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, c->KS, c->Gd))) return rc;
     } else {
@@ -2481,7 +2664,15 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     if ((rc = launch_row<real>(c, B, ROW_INIT0, 0, 0, G, Gb))) return rc;
   }
   for (int t = 0; t < T; ++t) {
-    if (dense) {
+    if (i8) {
+      // z -> digit planes -> Az GEMM (into the dense Az buffer, one partial)
+      // -> denoiser (+ beta digit planes) -> A beta GEMM (S8 partials)
+      if ((rc = i8_az(c, B, (float*)c->d_azp, (long long)c->lda))) return rc;
+      if ((rc = launch_dense_den(c, B, t, es, true))) return rc;
+      if ((rc = launch_gemm_i8<kI8NPB>(c, B, c->d_bq, c->LMp8, c->d_A8, c->np8, c->n, (float*)c->d_abp,
+                               (long long)S8 * c->n, c->n, S8, c->d_bfix + 1, 0, K_DAB)))
+        return rc;
+    } else if (dense) {
       if ((rc = launch_dense_az(c, B, t, es, 0))) return rc;
       if ((rc = launch_dense_den(c, B, t, es))) return rc;
       if ((rc = launch_dense_ab(c, B, t, es, 0))) return rc;
@@ -2580,6 +2771,8 @@ int set_power(sa_ctx* c, const double* Pl) {
     P += Pl[l];                                // np.sum(Pl), sparc_ldpc.py:190
   }
   c->P = P;
+  c->cmax = 0;
+  for (int l = 0; l < c->L; ++l) c->cmax = cl[l] > c->cmax ? cl[l] : c->cmax;
   int rc = upload(c, c->d_c, cl.data(), c->L);
   if (!rc) rc = upload(c, c->d_P1, &P, 1);
   if (rc) return rc;
@@ -2588,6 +2781,7 @@ int set_power(sa_ctx* c, const double* Pl) {
   c->pb_on = false;  // back to one allocation (graphs are keyed on the mode)
   c->shared_power = true;
   c->power_set = true;
+  if (c->d_bfix && (rc = i8_set_bfix(c))) return rc;
   return SA_OK;
 }
 
@@ -2727,6 +2921,12 @@ int set_lds_limits() {
     return fail(SA_ERR_HIP, "k_secb has static LDS: absolute LDS addressing in gather_step4 is invalid");
   hipError_t e = lds_attr_all<float>();
   if (e == hipSuccess) e = lds_attr_all<double>();
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_gemm_i8<kI8NPZ>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            I8Tile<kI8NPZ>::Lds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_gemm_i8<kI8NPB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            I8Tile<kI8NPB>::Lds);
   if (e != hipSuccess) return fail(SA_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
   done = 1;
   return SA_OK;
@@ -3122,6 +3322,8 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_fwd2);
   dev_free(c->d_fwd3);
   dev_free(c->d_A);
+  dev_free(c->d_A8); dev_free(c->d_AT8); dev_free(c->d_zq); dev_free(c->d_bq);
+  dev_free(c->d_zsc); dev_free(c->d_bsc0); dev_free(c->d_bfix);
   dev_free(c->d_c);
   dev_free(c->d_cd);
   dev_free(c->d_P1);
@@ -3159,7 +3361,7 @@ int sa_Az(sa_ctx* c, int B, const double* z, double* out) {
     rc = seq_az<double>(c, B);
   } else {
     rc = seq_az<float>(c, B);
-    if (!rc && c->backend == SA_BACKEND_DENSE) {
+    if (!rc && c->backend == SA_BACKEND_DENSE && !use_i8(c, B)) {
       k_dense_az_reduce<<<4096, 256, 0, c->stream>>>((const float*)c->d_azp, (float*)c->d_out, c->RS, c->lda, LM, B);
       HIP_TRY(hipGetLastError());
     }
@@ -3499,8 +3701,9 @@ int sa_plan(sa_ctx* c, int B, int64_t* o) {
   const bool dense = c->backend == SA_BACKEND_DENSE;
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
-  o[0] = dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? 5 : (c->sec4 ? 4 : 1)) : 0));
-  o[1] = dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
+  const bool i8 = use_i8(c, B);
+  o[0] = i8 ? 6 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? 5 : (c->sec4 ? 4 : 1)) : 0)));
+  o[1] = i8 ? i8_splits(c, B) : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
   o[3] = batched ? c->CB : 1;
   o[4] = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;

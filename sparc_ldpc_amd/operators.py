@@ -197,17 +197,20 @@ class SparcOperator:
     def last_run_ms(self) -> float:
         return float(self._lib.sa_run_event_ms(self._ctx))
 
-    KERNEL_KINDS = ("k_sec", "k_row", "k_dense_az", "k_dense_den", "k_dense_ab")
+    # kinds 2 / 4 are the int8 matrix-core GEMMs (k_gemm_i8) on the dense
+    # backend's batched path, the fp32 GEMVs below kI8MinB codewords
+    KERNEL_KINDS = ("k_sec", "k_row", "k_dense_az", "k_dense_den", "k_dense_ab", "k_i8_quant")
 
     def profile(self, B, T, early_stop=True, beta0=False, rep=1):
         """Eager decode with per-launch HIP events: {kind: (mean_ms, launches)}, total_ms.
         rep > 1: each launch issued rep times back to back between its events
         (mean = elapsed / rep; the staged results are then not a decode)."""
         flags = (0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP) | (_lib.SA_FLAG_BETA0 if beta0 else 0)
-        out = np.zeros(11)
+        nk = len(self.KERNEL_KINDS)
+        out = np.zeros(2 * nk + 1)
         check(self._lib.sa_profile_rep(self._ctx, int(B), int(T), flags, int(rep), dptr(out)))
         kinds = {k: (float(out[2 * i]), int(out[2 * i + 1])) for i, k in enumerate(self.KERNEL_KINDS)}
-        return kinds, float(out[10])
+        return kinds, float(out[2 * nk])
 
     def fetch(self, B):
         out = np.empty((B, self.L * self.M))
@@ -221,7 +224,7 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, None, it.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return it
 
-    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43")
+    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43", "dense_mfma")
 
     def fetch_z(self, B):
         """Residual z after the last decode's final iteration, (B, n)."""

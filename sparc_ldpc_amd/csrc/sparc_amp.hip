@@ -1301,8 +1301,17 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     const int bid = blockIdx.x, total = a.G * a.NC;
     if ((a.G & 7) == 0 && (total & 7) == 0) {
       const int x = bid & 7, j = bid >> 3;
+#ifndef SA_SECB_CHUNK_FAST
+      // the XCD's G/8 section groups fastest: the workgroups in flight on
+      // one XCD (two per CU) cover G/8 groups' tables and a few codeword
+      // chunks' z, which stay in its L2 together
+      const int gx = a.G >> 3;
+      g = (j % gx) * 8 + x;
+      chunk = j / gx;
+#else
       g = (j / a.NC) * 8 + x;
       chunk = j % a.NC;
+#endif
     } else {
       g = bid / a.NC;
       chunk = bid % a.NC;

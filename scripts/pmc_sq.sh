@@ -23,7 +23,7 @@ for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in sorted(acc.items()):
-    if not (k.startswith("k_sec") or k.startswith("k_row")):
+    if not k.startswith(("k_sec", "k_row", "k_gemm", "k_dense", "k_i8")):
         continue
     print(k, "(per launch, mean over launches; SQ_* cycle counters in quad-cycles)")
     for c, v in sorted(d.items()):

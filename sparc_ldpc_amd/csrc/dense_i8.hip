@@ -116,37 +116,67 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[p][j][i] = 0;
+  // the epilogue's per-codeword scales, loaded now so their latency hides
+  // behind the K loop (codeword of accumulator register i: see the epilogue)
+  const int h = lane >> 5;
+  double scl[4][4];
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = tx * kI8TX + wx * 32 + i + 8 * g4 + 4 * h;
+      scl[g4][i] = a.scale[(long long)(b < a.B ? b : 0) * a.sst];
+    }
 
   if (st0 < st1) {
     i8_stage_load<NP>(a, smem, tx, ty, (long long)st0 * kI8KS, wv, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  const int r31 = lane & 31, h = lane >> 5;
+  const int r31 = lane & 31;
+  // LDS byte offsets of this lane's operand rows (chunk c of row r at
+  // r * 128 + ((c ^ swz(r)) << 4)); the swizzle only depends on r
+  int xo[NP], yo[2], xz[NP], yz[2];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int r = p * kI8TX + wx * 32 + r31;
+    xo[p] = r * kI8KS;
+    xz[p] = i8_swz(r);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = wy * 64 + j * 32 + r31;
+    yo[j] = Tl::XR * kI8KS + r * kI8KS;
+    yz[j] = i8_swz(r);
+  }
   for (int st = st0; st < st1; ++st) {
     const int buf = (st - st0) & 1;
     if (st + 1 < st1)
       i8_stage_load<NP>(a, smem + (buf ^ 1) * Tl::Stage, tx, ty, (long long)(st + 1) * kI8KS, wv, lane);
-    const unsigned char* xs = smem + buf * Tl::Stage;
-    const unsigned char* ys = xs + Tl::XR * kI8KS;
+    const unsigned char* sb = smem + buf * Tl::Stage;
+    // operand fragments double-buffered across the four 32-deep K steps:
+    // step kk + 1's LDS reads are in flight while step kk's MFMAs issue
+    i8v4 xf[2][NP], yf[2][2];
 #pragma unroll
-    for (int kk = 0; kk < kI8KS / 32; ++kk) {
-      const int c = 2 * kk + h;  // this lane's 16-B chunk of the 32-deep K step
-      i8v4 xf[NP], yf[2];
+    for (int kk = 0; kk <= kI8KS / 32; ++kk) {
+      if (kk < kI8KS / 32) {
+        const int c = 2 * kk + h;  // this lane's 16-B chunk of the 32-deep K step
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int r = p * kI8TX + wx * 32 + r31;
-        xf[p] = *reinterpret_cast<const i8v4*>(xs + r * kI8KS + ((c ^ i8_swz(r)) << 4));
+        for (int p = 0; p < NP; ++p) xf[kk & 1][p] = *reinterpret_cast<const i8v4*>(sb + xo[p] + ((c ^ xz[p]) << 4));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) yf[kk & 1][j] = *reinterpret_cast<const i8v4*>(sb + yo[j] + ((c ^ yz[j]) << 4));
       }
+      // keep the reads above in front of the MFMAs below (the scheduler
+      // would otherwise sink them and wait for each group on the spot)
+      __builtin_amdgcn_sched_barrier(0);
+      if (kk > 0) {
+        const int q = (kk - 1) & 1;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wy * 64 + j * 32 + r31;
-        yf[j] = *reinterpret_cast<const i8v4*>(ys + r * kI8KS + ((c ^ i8_swz(r)) << 4));
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[p][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xf[q][p], yf[q][j], acc[p][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int p = 0; p < NP; ++p)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[p][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xf[p], yf[j], acc[p][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage's DMA has landed (this wave's)
     __syncthreads();                                   // ... every wave's, and this stage is consumed
@@ -164,7 +194,7 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
         double v = 0.0;
 #pragma unroll
         for (int p = 0; p < NP; ++p) v = v * 256.0 + (double)acc[p][j][i];
-        a.out[(long long)b * a.ldb + (long long)s * a.lds + y] = (float)(v * a.scale[(long long)b * a.sst]);
+        a.out[(long long)b * a.ldb + (long long)s * a.lds + y] = (float)(v * scl[i >> 2][i & 3]);
       }
     }
   }

@@ -1973,14 +1973,27 @@ __global__ void __launch_bounds__(256) k_dense_den(DenseArgs a, const float* c, 
     if (bq) {
       const double sf = bfix[0];
       int8_t* qb = bq + (long long)b * bq_ld + (long long)l * M;
+      if constexpr (E >= 4) {  // 4 consecutive elements per lane: one 4-byte store per plane
 #pragma unroll
-      for (int i = 0; i < E; ++i) {
-        const int e = elem_index<E>(lane, i);
-        if (e < M) {
-          int d[kI8NPB];
-          i8_digits<kI8NPB>((int)rint((double)v[i] * sf), d);
+        for (int i = 0; i < E; i += 4) {
+          const int e = elem_index<E>(lane, i);
+          int d[4][kI8NPB];
 #pragma unroll
-          for (int p = 0; p < kI8NPB; ++p) qb[p * bq_ps + e] = (int8_t)d[p];
+          for (int u = 0; u < 4; ++u) i8_digits<kI8NPB>((int)rint((double)v[i + u] * sf), d[u]);
+#pragma unroll
+          for (int p = 0; p < kI8NPB; ++p)
+            *reinterpret_cast<char4*>(qb + p * bq_ps + e) = make_char4(d[0][p], d[1][p], d[2][p], d[3][p]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+          const int e = elem_index<E>(lane, i);
+          if (e < M) {
+            int d[kI8NPB];
+            i8_digits<kI8NPB>((int)rint((double)v[i] * sf), d);
+#pragma unroll
+            for (int p = 0; p < kI8NPB; ++p) qb[p * bq_ps + e] = (int8_t)d[p];
+          }
         }
       }
     }

@@ -39,9 +39,12 @@ enum {
 
 enum {
   SA_BACKEND_HADAMARD = 0,  /* matrix-free sub-sampled Walsh-Hadamard operator (default) */
-  SA_BACKEND_DENSE = 1      /* materialised n x (L*M) design matrix: fp32 GEMVs for B < 4
+  SA_BACKEND_DENSE = 1,     /* materialised n x (L*M) design matrix: fp32 GEMVs for B < 4
                                codewords, int8 matrix-core GEMMs on exact +-1 entries with
                                three-digit fixed-point vectors for B >= 4 */
+  SA_BACKEND_HOST = 2       /* no device operator: the caller's own Ab / Az (any operator, as the
+                               reference's amp() accepts any callables) applied on the host, the
+                               loop's tau, denoiser and residual on the device (sa_host_*) */
 };
 
 enum { SA_PREC_F32 = 0, SA_PREC_F64 = 1 };
@@ -184,6 +187,26 @@ int sa_cancel(sa_ctx* ctx, int B, const int32_t* idx, sa_ctx* dst);
  * amp_test.py reps loop's hard initialisation (amp_test.py:207-210), where
  * beta_0 carries 1 = c_l / sqrt(n P / L) at the decided sections. */
 int sa_cancel_scaled(sa_ctx* ctx, int B, const int32_t* idx, double scale, sa_ctx* dst);
+
+/* ---- host-operator AMP (SA_BACKEND_HOST context; sa_create with ordering
+ * NULL) ------------------------------------------------------------------
+ * The reference's amp() takes ANY pair of callables (sparc_ldpc.py:189,196,
+ * 213,220).  For operators that are not this library's, the caller applies
+ * Ab / Az itself and the loop's other steps run on the device:
+ *   sa_host_init(B, T, y, Pl, beta0, Ab(beta0))  z = y - Ab(beta0) (:192-200; both NULL: zero start)
+ *   for t < T:
+ *     sa_host_tau(t, stopped)        tau_t = sqrt(sum z^2 / n), stopped[b] = (tau_t == tau_{t-1}) (:203-209)
+ *     if every codeword stopped: done
+ *     sa_fetch_z -> the caller computes Az(z)
+ *     sa_host_eta(t, Az(z))          beta = eta(beta + Az(z)) (:213-219)
+ *     sa_fetch -> the caller computes Ab(beta)
+ *     sa_host_residual(t, Ab(beta))  z = y - Ab(beta) + z / tau^2 (P - sum beta^2 / n) (:220)
+ * Stopped codewords keep beta and z.  flags: SA_FLAG_NO_EARLY_STOP. */
+int sa_host_init(sa_ctx* ctx, int B, int T, const double* y, const double* Pl, const double* beta0,
+                 const double* ab0);
+int sa_host_tau(sa_ctx* ctx, int B, int t, int flags, int* stopped);
+int sa_host_eta(sa_ctx* ctx, int B, int t, int flags, const double* az);
+int sa_host_residual(sa_ctx* ctx, int B, int t, int flags, const double* ab);
 
 /* Introspection. */
 /* The kernels a decode of B codewords runs: out8 = {section kernel (0 k_sec,

@@ -11,6 +11,8 @@ import sparc_ldpc_amd as sp
 from bench import WORKLOADS, n_of, synth_y
 
 w = dict(WORKLOADS[sys.argv[1] if len(sys.argv) > 1 else "c2"])
+if len(sys.argv) > 2:  # batch override (e.g. c4 1: the single-codeword k_sec43)
+    w["B"] = int(sys.argv[2])
 L, M, P, T, B = w["L"], w["M"], w["P"], w["T"], w["B"]
 n = n_of(w)
 Pl = P / L * np.ones(L)

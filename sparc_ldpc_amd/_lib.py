@@ -26,6 +26,7 @@ SA_ERR_NO_DEVICE = -6
 
 SA_BACKEND_HADAMARD = 0
 SA_BACKEND_DENSE = 1
+SA_BACKEND_HOST = 2
 SA_PREC_F32 = 0
 SA_PREC_F64 = 1
 SA_FLAG_NO_EARLY_STOP = 1
@@ -39,6 +40,7 @@ EXPORTS = (
     "sa_profile", "sa_profile_rep", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
     "sa_threshold", "sa_cancel", "sa_plan", "sa_stage_onehot_scaled", "sa_cancel_scaled",
+    "sa_host_init", "sa_host_tau", "sa_host_eta", "sa_host_residual",
 )
 
 _P = ct.c_void_p
@@ -76,6 +78,10 @@ _SIG = {
     "sa_llr": (_I, [_P, _I, _I, _I, _P, _I]),
     "sa_soft_beta0": (_I, [_P, _I, _I, _I, _P, _I]),
     "sa_hard_cancel": (_I, [_P, _I, _I, _I, _P, _I, _P, ct.POINTER(ct.c_int32)]),
+    "sa_host_init": (_I, [_P, _I, _I, _D, _D, _D, _D]),
+    "sa_host_tau": (_I, [_P, _I, _I, _I, ct.POINTER(ct.c_int)]),
+    "sa_host_eta": (_I, [_P, _I, _I, _I, _D]),
+    "sa_host_residual": (_I, [_P, _I, _I, _I, _D]),
 }
 
 _lib = None

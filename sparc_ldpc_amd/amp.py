@@ -3,16 +3,19 @@ ldpc/amp_test.py:14-50, running the whole iteration loop on the MI355X.
 
 ``amp(y, σ_n, Pl, L, M, T, Ab, Az, β)`` keeps the reference's positional
 order (every call site is positional: sparc_ldpc.py:449,524,637,698,796,846,
-954,1017; amp_exit.py:238; amp_test.py:214,231,240).  ``Ab``/``Az`` must be
-the operator objects returned by this package's ``sparc_transforms`` /
-``sparc_transforms_shorter`` (the only operators any reference call site
-passes); arbitrary Python callables are rejected rather than run on the CPU.
+954,1017; amp_exit.py:238; amp_test.py:214,231,240).  With the operator
+objects of this package's ``sparc_transforms`` / ``sparc_transforms_shorter``
+(what every reference call site passes) the whole loop runs on the device.
+Like the reference, ``amp`` also accepts any other pair of callables: those
+are the caller's operator and run where the caller wrote them, while τ, the
+exact-τ stop, η and the Onsager residual still run on the device
+(``HostOperatorLoop``, binary64).
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .operators import AbOp, AzOp, SparcOperator
+from .operators import AbOp, AzOp, SparcOperator, host_loop
 
 __all__ = ["amp", "amp_test", "amp_batch", "operator_of"]
 
@@ -50,6 +53,14 @@ def _beta0(β, L, M):
 
 
 def _run(y, Pl, L, M, T, Ab, Az, β, early_stop):
+    if not (isinstance(Ab, AbOp) and isinstance(Az, AzOp) and Ab.op is Az.op):
+        # the caller's own operator (sparc_ldpc.py:189 takes any callables)
+        if not (callable(Ab) and callable(Az)):
+            raise TypeError(f"Ab and Az must be callable; got {type(Ab).__name__}/{type(Az).__name__}")
+        y = np.asarray(y, dtype=np.float64)
+        loop = host_loop(L, M, y.size)
+        b, it = loop.run(y, Pl, T, Ab, Az, _beta0(β, L, M), early_stop)
+        return b, it
     op = operator_of(Ab, Az)
     assert L == op.L and M == op.M, "L, M must match the operator"
     y = np.asarray(y, dtype=np.float64)

@@ -1937,39 +1937,50 @@ __global__ void __launch_bounds__(256) k_dense_ab(DenseArgs a, const float* tau)
 // On the int8 matrix-core path (bq != NULL) it also writes the new beta's
 // kI8NPB base-256 digit planes at the fixed scale bfix[0] (beta_l <= c_l, so
 // one power-of-two scale per decode: dense_i8.hip).
-template <int E>
-__global__ void __launch_bounds__(256) k_dense_den(DenseArgs a, const float* c, float* beta,
-                                                   float* bbp, float* tau_out, int* iters, int G,
+// Also the denoiser of the host-operator path (SA_BACKEND_HOST: the caller's
+// A^T z uploaded as the single partial), in either precision.
+template <typename real>
+struct DenArgs {
+  const real* azp;  // [B][RS][lda] A^T z partials (scaled: A carries 1/sqrt(n))
+  const real* zzp;  // [B][NZ]
+  const real* tau;  // [B][T1]
+  int L, M, n, NZ, T1, t, early_stop, RS;
+  size_t lda;
+};
+
+template <typename real, int E>
+__global__ void __launch_bounds__(256) k_dense_den(DenArgs<real> a, const real* c, real* beta,
+                                                   real* bbp, real* tau_out, int* iters, int G,
                                                    int8_t* bq, long long bq_ps, long long bq_ld,
                                                    const double* bfix) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = blockIdx.x, b = blockIdx.y;
   const int l = g * 4 + wv;
   const int M = a.M;
-  const float tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, a.n);
-  const float last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : 0.f;
+  const real tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, a.n);
+  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
   const bool stop = a.early_stop && tau == last;
   if (g == 0 && threadIdx.x == 0) {
     tau_out[(size_t)b * a.T1 + a.t] = tau;
     if (stop && iters[b] < 0) iters[b] = a.t;
   }
   if (stop) return;
-  __shared__ float bbw[4];
-  float bb = 0.f;
+  __shared__ real bbw[4];
+  real bb = 0;
   if (l < a.L) {
-    float v[E];
+    real v[E];
 #pragma unroll
     for (int i = 0; i < E; ++i) {
       const int e = elem_index<E>(lane, i);
-      float s = 0.f;
+      real s = 0;
       if (e < M)
         for (int rs = 0; rs < a.RS; ++rs) s += a.azp[((size_t)b * a.RS + rs) * a.lda + (size_t)l * M + e];
       v[i] = s;  // already carries the 1/sqrt(n) of A
     }
-    float* bl = beta + ((size_t)b * a.L + l) * M;
-    float bprev[E];
-    load_section<float, E>(bl, bprev, lane, M);
-    bb = denoise_section<float, E>(v, bprev, bl, lane, M, c[l], tau * tau, 1.0f);
+    real* bl = beta + ((size_t)b * a.L + l) * M;
+    real bprev[E];
+    load_section<real, E>(bl, bprev, lane, M);
+    bb = denoise_section<real, E>(v, bprev, bl, lane, M, c[l], tau * tau, (real)1);
     if (bq) {
       const double sf = bfix[0];
       int8_t* qb = bq + (long long)b * bq_ld + (long long)l * M;
@@ -2002,9 +2013,25 @@ __global__ void __launch_bounds__(256) k_dense_den(DenseArgs a, const float* c, 
   __syncthreads();
   if (threadIdx.x == 0) {
     const int ns = min(4, a.L - g * 4);
-    float t = 0.f;
+    real t = 0;
     for (int s = 0; s < ns; ++s) t += bbw[s];
     bbp[(size_t)b * G + g] = t;
+  }
+}
+
+// tau_t of the host-operator loop (sparc_ldpc.py:203-209), ahead of the
+// caller's A^T z: tau[b][t], the exact tau == last_tau stop and stopped[b].
+template <typename real>
+__global__ void __launch_bounds__(64) k_tau(const real* zzp, int NZ, int n, real* tau, int T1, int t,
+                                            int early_stop, int* iters, int* stopped) {
+  const int b = blockIdx.x;
+  const real tv = tau_from_parts(zzp + (size_t)b * NZ, NZ, n);
+  if (threadIdx.x == 0) {
+    const real last = t > 0 ? tau[(size_t)b * T1 + t - 1] : (real)0;
+    const bool stop = early_stop && tv == last;
+    tau[(size_t)b * T1 + t] = tv;
+    if (stop && iters[b] < 0) iters[b] = t;
+    stopped[b] = stop ? 1 : 0;
   }
 }
 
@@ -2085,6 +2112,7 @@ struct sa_ctx {
   void *d_y = nullptr, *d_z = nullptr, *d_beta = nullptr, *d_out = nullptr, *d_abp = nullptr;
   void *d_bbp = nullptr, *d_zzp = nullptr, *d_tau = nullptr, *d_c = nullptr, *d_azp = nullptr;
   int* d_iters = nullptr;
+  int* d_stop = nullptr;  // host-operator loop: codewords whose exact-tau stop fired
   int32_t* d_idx = nullptr;
   double* d_stage = nullptr;
   size_t stage_cap = 0;
@@ -2136,6 +2164,7 @@ void free_workspace(sa_ctx* c) {
     *p = nullptr;
   }
   dev_free(c->d_iters); c->d_iters = nullptr;
+  dev_free(c->d_stop); c->d_stop = nullptr;
   dev_free(c->d_idx); c->d_idx = nullptr;
   dev_free(c->d_beta2); c->d_beta2 = nullptr;
   c->beta2_cap = 0;
@@ -2255,11 +2284,14 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZ16 * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_tau, (size_t)nB * (nT + 1) * s))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_iters, (size_t)nB * sizeof(int)))) return rc;
+  if ((rc = dev_alloc(c, (void**)&c->d_stop, (size_t)nB * sizeof(int)))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_idx, (size_t)nB * c->L * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, &c->d_cb, (size_t)nB * c->L * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_Pb, (size_t)nB * s))) return rc;
   if (c->backend == SA_BACKEND_DENSE)
     if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->RS * c->lda * sizeof(float)))) return rc;
+  if (c->backend == SA_BACKEND_HOST)  // the caller's A^T z, one partial per codeword
+    if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->lda * s))) return rc;
   c->Bcap = nB;
   c->Tcap = nT;
   // Debug aid: SPARC_AMP_POISON=<mask> fills the workspace with 0xFF bytes
@@ -2345,7 +2377,7 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb
   a.Gb = Gb; a.T1 = c->Tcap + 1; a.t = t; a.mode = mode;
   a.early_stop = early_stop;
   // the dense matrix already carries the 1/sqrt(n) of sparc_ldpc.py:143-146
-  a.sqrt_n = c->backend == SA_BACKEND_DENSE ? (real)1 : (real)std::sqrt((double)c->n);
+  a.sqrt_n = c->backend != SA_BACKEND_HADAMARD ? (real)1 : (real)std::sqrt((double)c->n);
   a.Pb = c->pb_on ? (const real*)c->d_Pb : (const real*)c->d_P1;
   a.Pbst = c->pb_on ? 1 : 0;
   return a;
@@ -2531,30 +2563,35 @@ int launch_dense_ab(sa_ctx* c, int B, int t, int es, int mode) {
   return SA_OK;
 }
 
-template <int E>
-void launch_dense_den_e(sa_ctx* c, int B, const DenseArgs& a, bool i8) {
+template <typename real, int E>
+void launch_dense_den_e(sa_ctx* c, int B, const DenArgs<real>& a, bool i8) {
   dim3 grid(c->Gd, B);
   if (c->prof) c->prof->begin(c->stream, K_DDEN);
-  PROF_REPS(c) k_dense_den<E><<<grid, 256, 0, c->stream>>>(a, (const float*)c->d_c, (float*)c->d_beta,
-                                               (float*)c->d_bbp, (float*)c->d_tau, c->d_iters, c->Gd,
+  PROF_REPS(c) k_dense_den<real, E><<<grid, 256, 0, c->stream>>>(a, (const real*)c->d_c, (real*)c->d_beta,
+                                               (real*)c->d_bbp, (real*)c->d_tau, c->d_iters, c->Gd,
                                                i8 ? c->d_bq : nullptr, (long long)c->Bp8 * c->LMp8,
                                                c->LMp8, c->d_bfix);
   if (c->prof) c->prof->end(c->stream);
 }
 
 // i8 = true: the Az of the matrix-core GEMM (one partial, d_azp[b][0][:]) and
-// the beta digit planes written for the next A beta GEMM
+// the beta digit planes written for the next A beta GEMM.  The host-operator
+// backend's A^T z is one uploaded partial as well.
+template <typename real = float>
 int launch_dense_den(sa_ctx* c, int B, int t, int es, bool i8 = false) {
-  DenseArgs a = dense_args(c, t, es, 0);
-  if (i8) a.RS = 1;
+  DenArgs<real> a;
+  a.azp = (const real*)c->d_azp; a.zzp = (const real*)c->d_zzp; a.tau = (const real*)c->d_tau;
+  a.L = c->L; a.M = c->M; a.n = c->n; a.NZ = c->nz_cur; a.T1 = c->Tcap + 1; a.t = t; a.early_stop = es;
+  a.RS = (i8 || c->backend == SA_BACKEND_HOST) ? 1 : c->RS;
+  a.lda = c->lda;
   switch (c->E) {
-    case 1: launch_dense_den_e<1>(c, B, a, i8); break;
-    case 2: launch_dense_den_e<2>(c, B, a, i8); break;
-    case 4: launch_dense_den_e<4>(c, B, a, i8); break;
-    case 8: launch_dense_den_e<8>(c, B, a, i8); break;
-    case 16: launch_dense_den_e<16>(c, B, a, i8); break;
-    case 32: launch_dense_den_e<32>(c, B, a, i8); break;
-    case 64: launch_dense_den_e<64>(c, B, a, i8); break;
+    case 1: launch_dense_den_e<real, 1>(c, B, a, i8); break;
+    case 2: launch_dense_den_e<real, 2>(c, B, a, i8); break;
+    case 4: launch_dense_den_e<real, 4>(c, B, a, i8); break;
+    case 8: launch_dense_den_e<real, 8>(c, B, a, i8); break;
+    case 16: launch_dense_den_e<real, 16>(c, B, a, i8); break;
+    case 32: launch_dense_den_e<real, 32>(c, B, a, i8); break;
+    case 64: launch_dense_den_e<real, 64>(c, B, a, i8); break;
     default: return fail(SA_ERR_UNSUPPORTED, "bad E");
   }
   HIP_TRY(hipGetLastError());
@@ -2783,6 +2820,15 @@ int check_ctx(const sa_ctx* c) {
   return SA_OK;
 }
 
+// Entry points that apply the design operator on the device: not on a
+// host-operator context (SA_BACKEND_HOST holds no operator).
+int check_op(const sa_ctx* c, const char* what) {
+  if (!c) return fail(SA_ERR_ARG, "null context");
+  if (c->backend == SA_BACKEND_HOST)
+    return fail(SA_ERR_UNSUPPORTED, std::string(what) + ": a host-operator context has no device operator");
+  return SA_OK;
+}
+
 int set_power(sa_ctx* c, const double* Pl) {
   if (!Pl) return fail(SA_ERR_ARG, "Pl is NULL");
   std::vector<double> cl(c->L);
@@ -2958,8 +3004,10 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
                 int device) {
   if (!out) return fail(SA_ERR_ARG, "out is NULL");
   *out = nullptr;
-  if (L <= 0 || M <= 0 || n <= 0 || !ordering) return fail(SA_ERR_ARG, "L, M, n must be positive and ordering non-NULL");
-  if (backend != SA_BACKEND_HADAMARD && backend != SA_BACKEND_DENSE) return fail(SA_ERR_ARG, "unknown backend");
+  if (L <= 0 || M <= 0 || n <= 0) return fail(SA_ERR_ARG, "L, M, n must be positive");
+  if (backend != SA_BACKEND_HADAMARD && backend != SA_BACKEND_DENSE && backend != SA_BACKEND_HOST)
+    return fail(SA_ERR_ARG, "unknown backend");
+  if (!ordering && backend != SA_BACKEND_HOST) return fail(SA_ERR_ARG, "ordering is NULL");
   if (prec != SA_PREC_F32 && prec != SA_PREC_F64) return fail(SA_ERR_ARG, "unknown precision");
   if (backend == SA_BACKEND_DENSE && prec != SA_PREC_F32)
     return fail(SA_ERR_UNSUPPORTED, "dense backend streams an fp32 matrix (precision must be F32)");
@@ -2977,7 +3025,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   c->w = 1 << ilog2(mx);  // 2^ceil(log2(max(M+1, n+1))), sparc_ldpc.py:52/:110
   c->nhi = c->w / M;
   c->E = M >= 64 ? M / 64 : 1;
-  c->ordering.assign(ordering, ordering + (size_t)L * n);
+  if (ordering) c->ordering.assign(ordering, ordering + (size_t)L * n);
   c->NZ = (n + kRowsPerBlk - 1) / kRowsPerBlk;
   c->NZ16 = (n + kRow2Rows - 1) / kRow2Rows;
   c->nz_cur = c->NZ;
@@ -3051,6 +3099,8 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     c->KS = 8;
     rc = build_tables(c);  // validates the ordering (distinct values in [1, w))
     if (!rc) rc = build_dense(c);
+  } else if (backend == SA_BACKEND_HOST) {
+    c->lda = (size_t)L * M;  // no operator on the device: the caller's products are uploaded
   } else {
     rc = build_tables(c);
   }
@@ -3320,7 +3370,7 @@ int sa_create(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int b
 }
 
 int sa_subset(const sa_ctx* parent, const int64_t* sections, int Ls, sa_ctx** out) {
-  if (check_ctx(parent)) return SA_ERR_ARG;
+  if (int rc0 = check_op(parent, "sa_subset")) return rc0;
   if (!sections || Ls <= 0) return fail(SA_ERR_ARG, "empty section subset");
   std::vector<uint32_t> ord((size_t)Ls * parent->n);
   for (int i = 0; i < Ls; ++i) {
@@ -3357,7 +3407,7 @@ void sa_destroy(sa_ctx* c) {
 }
 
 int sa_Ab(sa_ctx* c, int B, const double* beta, double* out) {
-  if (check_ctx(c)) return SA_ERR_ARG;
+  if (int rc0 = check_op(c, "sa_Ab")) return rc0;
   if (B <= 0 || !beta || !out) return fail(SA_ERR_ARG, "sa_Ab: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
@@ -3372,7 +3422,7 @@ int sa_Ab(sa_ctx* c, int B, const double* beta, double* out) {
 }
 
 int sa_Az(sa_ctx* c, int B, const double* z, double* out) {
-  if (check_ctx(c)) return SA_ERR_ARG;
+  if (int rc0 = check_op(c, "sa_Az")) return rc0;
   if (B <= 0 || !z || !out) return fail(SA_ERR_ARG, "sa_Az: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
@@ -3423,7 +3473,7 @@ int sa_stage_power_batch(sa_ctx* c, int B, const double* Pl) {
 }
 
 int sa_run(sa_ctx* c, int B, int T, int flags) {
-  if (check_ctx(c)) return SA_ERR_ARG;
+  if (int rc0 = check_op(c, "sa_run")) return rc0;
   if (B <= 0 || T < 0) return fail(SA_ERR_ARG, "sa_run: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_run: power allocation not staged");
   if (B > c->Bcap) return fail(SA_ERR_ARG, "sa_run: batch larger than the staged batch");
@@ -3461,6 +3511,89 @@ int sa_fetch_z(sa_ctx* c, int B, double* z_out) {
   return SA_OK;
 }
 
+// ---- host-operator AMP (SA_BACKEND_HOST): the caller's Ab / Az ----------
+extern "C++" {
+namespace {
+int check_host(sa_ctx* c, int B, const char* what) {
+  if (!c) return fail(SA_ERR_ARG, "null context");
+  if (c->backend != SA_BACKEND_HOST)
+    return fail(SA_ERR_UNSUPPORTED, std::string(what) + ": needs a host-operator context (SA_BACKEND_HOST)");
+  if (B <= 0 || B > c->Bcap) return fail(SA_ERR_ARG, std::string(what) + ": bad batch (sa_host_init first)");
+  return SA_OK;
+}
+
+template <typename real>
+int host_init_impl(sa_ctx* c, int B, const double* beta0, const double* ab0) {
+  int rc;
+  c->nz_cur = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;
+  k_fill32<<<(B + 255) / 256, 256, 0, c->stream>>>((uint32_t*)c->d_iters, 0xffffffffu, (size_t)B);
+  if (beta0) {  // z = y - Ab(beta0) with the caller's Ab(beta0) (sparc_ldpc.py:196-200)
+    if ((rc = upload(c, c->d_beta, beta0, (size_t)B * c->L * c->M))) return rc;
+    if ((rc = upload(c, c->d_abp, ab0, (size_t)B * c->n))) return rc;
+    return launch_row<real>(c, B, ROW_INIT, 0, 0, 1, c->Gd);
+  }
+  const size_t nw = (size_t)B * c->L * c->M * rsz(c) / 4;
+  k_fill32<<<(int)std::min<size_t>((nw + 255) / 256, 8192), 256, 0, c->stream>>>((uint32_t*)c->d_beta, 0u, nw);
+  return launch_row<real>(c, B, ROW_INIT0, 0, 0, 1, c->Gd);
+}
+}  // namespace
+}  // extern "C++"
+
+int sa_host_init(sa_ctx* c, int B, int T, const double* y, const double* Pl, const double* beta0, const double* ab0) {
+  if (!c) return fail(SA_ERR_ARG, "null context");
+  if (c->backend != SA_BACKEND_HOST) return fail(SA_ERR_UNSUPPORTED, "sa_host_init: needs a host-operator context");
+  if (B <= 0 || T < 0 || !y || !Pl || (!beta0) != (!ab0))
+    return fail(SA_ERR_ARG, "sa_host_init: bad arguments (beta0 and Ab(beta0) go together)");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = ensure_workspace(c, B, T > 0 ? T : 1);
+  if (!rc) rc = set_power(c, Pl);
+  if (!rc) rc = upload(c, c->d_y, y, (size_t)B * c->n);
+  if (rc) return rc;
+  rc = c->prec == SA_PREC_F64 ? host_init_impl<double>(c, B, beta0, ab0) : host_init_impl<float>(c, B, beta0, ab0);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
+int sa_host_tau(sa_ctx* c, int B, int t, int flags, int* stopped) {
+  if (int rc = check_host(c, B, "sa_host_tau")) return rc;
+  if (t < 0 || t >= c->Tcap || !stopped) return fail(SA_ERR_ARG, "sa_host_tau: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  const int es = (flags & SA_FLAG_NO_EARLY_STOP) ? 0 : 1;
+  if (c->prec == SA_PREC_F64)
+    k_tau<double><<<B, 64, 0, c->stream>>>((const double*)c->d_zzp, c->nz_cur, c->n, (double*)c->d_tau, c->Tcap + 1,
+                                            t, es, c->d_iters, c->d_stop);
+  else
+    k_tau<float><<<B, 64, 0, c->stream>>>((const float*)c->d_zzp, c->nz_cur, c->n, (float*)c->d_tau, c->Tcap + 1,
+                                           t, es, c->d_iters, c->d_stop);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(stopped, c->d_stop, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
+int sa_host_eta(sa_ctx* c, int B, int t, int flags, const double* az) {
+  if (int rc = check_host(c, B, "sa_host_eta")) return rc;
+  if (t < 0 || t >= c->Tcap || !az) return fail(SA_ERR_ARG, "sa_host_eta: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  const int es = (flags & SA_FLAG_NO_EARLY_STOP) ? 0 : 1;
+  int rc = upload(c, c->d_azp, az, (size_t)B * c->L * c->M);
+  if (!rc) rc = c->prec == SA_PREC_F64 ? launch_dense_den<double>(c, B, t, es) : launch_dense_den<float>(c, B, t, es);
+  return rc;
+}
+
+int sa_host_residual(sa_ctx* c, int B, int t, int flags, const double* ab) {
+  if (int rc = check_host(c, B, "sa_host_residual")) return rc;
+  if (t < 0 || t >= c->Tcap || !ab) return fail(SA_ERR_ARG, "sa_host_residual: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  const int es = (flags & SA_FLAG_NO_EARLY_STOP) ? 0 : 1;
+  int rc = upload(c, c->d_abp, ab, (size_t)B * c->n);
+  if (!rc)
+    rc = c->prec == SA_PREC_F64 ? launch_row<double>(c, B, ROW_AMP, t, es, 1, c->Gd)
+                                : launch_row<float>(c, B, ROW_AMP, t, es, 1, c->Gd);
+  return rc;
+}
+
 int sa_fetch(sa_ctx* c, int B, double* beta_out, int* iters_out) {
   if (check_ctx(c)) return SA_ERR_ARG;
   if (B <= 0 || B > c->Bcap) return fail(SA_ERR_ARG, "sa_fetch: bad batch");
@@ -3474,7 +3607,7 @@ int sa_fetch(sa_ctx* c, int B, double* beta_out, int* iters_out) {
 
 int sa_amp(sa_ctx* c, int B, const double* y, const double* Pl, int T, const double* beta0, double* beta_out,
            int* iters_out, int flags) {
-  if (check_ctx(c)) return SA_ERR_ARG;
+  if (int rc0 = check_op(c, "sa_amp")) return rc0;
   if (B <= 0 || T < 0 || !y || !Pl || !beta_out) return fail(SA_ERR_ARG, "sa_amp: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, T > 0 ? T : 1);
@@ -3493,7 +3626,7 @@ int sa_amp(sa_ctx* c, int B, const double* y, const double* Pl, int T, const dou
 int sa_profile(sa_ctx* c, int B, int T, int flags, double* out) { return sa_profile_rep(c, B, T, flags, 1, out); }
 
 int sa_profile_rep(sa_ctx* c, int B, int T, int flags, int rep, double* out) {
-  if (check_ctx(c)) return SA_ERR_ARG;
+  if (int rc0 = check_op(c, "sa_profile")) return rc0;
   if (B <= 0 || T <= 0 || !out || B > c->Bcap || T > c->Tcap || !c->power_set || rep < 1 || rep > 1024)
     return fail(SA_ERR_ARG, "sa_profile: bad arguments (reserve and stage first)");
   HIP_TRY(hipSetDevice(c->device));
@@ -3560,7 +3693,7 @@ int sa_encode(sa_ctx* c, int B, const int32_t* idx, const double* noise) {
   if (check_ctx(c)) return SA_ERR_ARG;
   if (B <= 0 || !idx) return fail(SA_ERR_ARG, "sa_encode: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_encode: power allocation not staged");
-  if (c->backend != SA_BACKEND_HADAMARD && c->backend != SA_BACKEND_DENSE) return fail(SA_ERR_ARG, "backend");
+  if (int rc0 = check_op(c, "sa_encode")) return rc0;
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
   if (rc) return rc;
@@ -3655,6 +3788,7 @@ int sa_soft_beta0(sa_ctx* c, int B, int l0, int ns, const double* app, int flags
 }
 
 int sa_hard_cancel(sa_ctx* c, int B, int l0, int ns, const double* app, int flags, sa_ctx* dst, int32_t* idx_out) {
+  if (dst && check_op(c, "sa_hard_cancel")) return SA_ERR_UNSUPPORTED;
   int rc = check_glue(c, B, l0, ns);
   if (rc) return rc;
   if (!app) return fail(SA_ERR_ARG, "sa_hard_cancel: app is NULL");
@@ -3697,6 +3831,7 @@ int sa_threshold(sa_ctx* c, int B, int l0, int ns, const double* app, int flags,
 
 int sa_cancel_scaled(sa_ctx* c, int B, const int32_t* idx, double scale, sa_ctx* dst) {
   if (check_ctx(c) || check_ctx(dst)) return SA_ERR_ARG;
+  if (int rc0 = check_op(c, "sa_cancel")) return rc0;
   if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_cancel: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_cancel: power allocation not staged");
   if (dst->n != c->n || dst->prec != c->prec || dst->device != c->device)

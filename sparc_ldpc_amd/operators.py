@@ -19,7 +19,7 @@ from . import _lib
 from ._lib import as_f64, check, dptr
 
 __all__ = [
-    "SparcOperator", "AbOp", "AzOp", "make_ordering", "sub_fht", "block_sub_fht",
+    "SparcOperator", "AbOp", "AzOp", "HostOperatorLoop", "make_ordering", "sub_fht", "block_sub_fht",
     "sparc_transforms", "sparc_transforms_shorter", "default_device",
 ]
 
@@ -348,6 +348,91 @@ class SparcOperator:
         sec = np.ascontiguousarray(np.asarray(sections, dtype=np.int64).reshape(-1))
         return SparcOperator(len(sec), self.M, self.n, self.ordering[sec],
                              self.backend, self.precision, self.device)
+
+
+class HostOperatorLoop:
+    """The AMP loop for operators that are not this package's
+    (``amp(y, σ, Pl, L, M, T, Ab, Az)`` with any callables, as the reference's
+    amp() accepts, sparc_ldpc.py:189-222): the caller's ``Ab``/``Az`` run where
+    the caller wrote them; τ, the exact-τ stop, the section denoiser η and the
+    Onsager residual run on the device in binary64 (an ``SA_BACKEND_HOST``
+    context, ``sa_host_*`` in include/sparc_amp.h).  One codeword per call,
+    the callables invoked exactly as often, and with the same shapes ((n, 1)
+    and (L·M, 1) float64), as in the reference loop.
+    """
+
+    def __init__(self, L, M, n, precision="fp64", device=None):
+        lib = _lib.load()
+        self.L, self.M, self.n = int(L), int(M), int(n)
+        self.precision = precision
+        self.device = default_device() if device is None else int(device)
+        self._ctx = _lib.ct.c_void_p()
+        check(lib.sa_create(_lib.ct.byref(self._ctx), self.L, self.M, self.n, None, _lib.SA_BACKEND_HOST,
+                            _PRECS[precision], self.device))
+        self._lib = lib
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.value:
+            try:
+                self._lib.sa_destroy(ctx)
+            except Exception:
+                pass
+            self._ctx = None
+
+    def run(self, y, Pl, T, Ab, Az, beta0=None, early_stop=True):
+        """-> (β̂ (L·M, 1), t): t = the loop index at which the exact-τ stop
+        fired (sparc_ldpc.py:204), or T when the loop ran out."""
+        L, M, n, lib = self.L, self.M, self.n, self._lib
+        y = as_f64(y).reshape(-1)
+        assert y.size == n, "y must be n long"
+        Pl = as_f64(Pl).reshape(-1)
+        assert Pl.size == L, "Pl must hold one power per section"
+        ab0 = None
+        if beta0 is not None:
+            beta0 = as_f64(beta0).reshape(-1)
+            ab0 = as_f64(Ab(beta0.reshape(-1, 1))).reshape(-1)  # sparc_ldpc.py:198
+            assert ab0.size == n, "Ab must return n values"
+        check(lib.sa_host_init(self._ctx, 1, int(T), dptr(y), dptr(Pl), None if beta0 is None else dptr(beta0),
+                               None if ab0 is None else dptr(ab0)))
+        flags = 0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP
+        stopped = np.zeros(1, dtype=np.int32)
+        z = np.empty((1, n))
+        beta = np.empty((1, L * M))
+        t_stop = int(T)
+        for t in range(int(T)):
+            check(lib.sa_host_tau(self._ctx, 1, t, flags, stopped.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
+            if stopped[0]:
+                t_stop = t
+                break
+            check(lib.sa_fetch_z(self._ctx, 1, dptr(z)))
+            az = as_f64(Az(z.reshape(-1, 1))).reshape(-1)                  # :213
+            assert az.size == L * M, "Az must return L*M values"
+            check(lib.sa_host_eta(self._ctx, 1, t, flags, dptr(az)))
+            check(lib.sa_fetch(self._ctx, 1, dptr(beta), None))
+            ab = as_f64(Ab(beta.reshape(-1, 1))).reshape(-1)               # :220
+            assert ab.size == n, "Ab must return n values"
+            check(lib.sa_host_residual(self._ctx, 1, t, flags, dptr(ab)))
+        check(lib.sa_fetch(self._ctx, 1, dptr(beta), None))
+        return beta.reshape(-1, 1), t_stop
+
+
+_HOST_LOOPS: "OrderedDict[tuple, HostOperatorLoop]" = OrderedDict()
+
+
+def host_loop(L, M, n, device=None) -> HostOperatorLoop:
+    """A cached host-operator loop context for (L, M, n)."""
+    dev = default_device() if device is None else int(device)
+    key = (int(L), int(M), int(n), dev)
+    hit = _HOST_LOOPS.get(key)
+    if hit is None:
+        hit = HostOperatorLoop(L, M, n, device=dev)
+        _HOST_LOOPS[key] = hit
+        while len(_HOST_LOOPS) > 4:
+            _HOST_LOOPS.popitem(last=False)
+    else:
+        _HOST_LOOPS.move_to_end(key)
+    return hit
 
 
 class AbOp:

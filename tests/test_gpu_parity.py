@@ -224,9 +224,11 @@ def test_amp_edge_cases(sp):
         Az(np.zeros(n - 1))
     with pytest.raises(AssertionError):
         sp.amp(np.zeros(n + 1), 0, Pl, L, M, 3, Ab, Az)
-    # foreign callables are rejected, never run on the CPU
-    with pytest.raises(TypeError):
+    # the caller's own callables must return the reference's shapes
+    with pytest.raises(AssertionError):
         sp.amp(y, 0, Pl, L, M, 3, lambda b: b, lambda z: z)
+    with pytest.raises(TypeError):
+        sp.amp(y, 0, Pl, L, M, 3, Ab, None)
     # bad orderings are rejected by the library
     bad = np.tile(np.arange(1, n + 1, dtype=np.uint32), (L, 1))
     bad[0, 1] = bad[0, 0]

@@ -102,10 +102,12 @@ def test_beta0_sentinels():
         _beta0(np.zeros(7), 2, 4)
 
 
-def test_amp_rejects_foreign_operators():
+def test_amp_rejects_non_callable_operators():
+    """amp() takes any callables (sparc_ldpc.py:189); anything else is a
+    TypeError before the device is touched."""
     import sparc_ldpc_amd as sp
     with pytest.raises(TypeError):
-        sp.amp(np.zeros(8), 0, np.ones(2), 2, 4, 3, lambda b: b, lambda z: z)
+        sp.amp(np.zeros(8), 0, np.ones(2), 2, 4, 3, "Ab", None)
 
 
 # ---- Monte-Carlo stopping rule and sharding --------------------------------

@@ -379,6 +379,42 @@ __device__ __forceinline__ void store_section(real* p, const real (&x)[E], int l
   }
 }
 
+// The same for any M (the dense and host-operator backends accept M that is
+// not a power of two, like the reference's sub_fht, sparc_ldpc.py:32-79):
+// 16-B vectors only where the four elements exist and the section is 16-B
+// aligned, element by element otherwise.
+template <typename real, int E>
+__device__ __forceinline__ void load_section_any(const real* p, real (&x)[E], int lane, int M) {
+  constexpr int Q = E < 4 ? E : 4;
+#pragma unroll
+  for (int i = 0; i < E; i += Q) {
+    const int e0 = elem_index<E>(lane, i);
+    if (Q == 4 && sizeof(real) == 4 && (M & 3) == 0 && e0 + 4 <= M) {
+      const float4 t = *reinterpret_cast<const float4*>(p + e0);
+      x[i] = t.x; x[i + 1] = t.y; x[i + 2] = t.z; x[i + 3] = t.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) x[i + q] = e0 + q < M ? p[e0 + q] : (real)0;
+    }
+  }
+}
+
+template <typename real, int E>
+__device__ __forceinline__ void store_section_any(real* p, const real (&x)[E], int lane, int M) {
+  constexpr int Q = E < 4 ? E : 4;
+#pragma unroll
+  for (int i = 0; i < E; i += Q) {
+    const int e0 = elem_index<E>(lane, i);
+    if (Q == 4 && sizeof(real) == 4 && (M & 3) == 0 && e0 + 4 <= M) {
+      *reinterpret_cast<float4*>(p + e0) = make_float4(x[i], x[i + 1], x[i + 2], x[i + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (e0 + q < M) p[e0 + q] = x[i + q];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Matrix-free Hadamard backend
 // ---------------------------------------------------------------------------
@@ -1979,15 +2015,17 @@ __global__ void __launch_bounds__(256) k_dense_den(DenArgs<real> a, const real* 
     }
     real* bl = beta + ((size_t)b * a.L + l) * M;
     real bprev[E];
-    load_section<real, E>(bl, bprev, lane, M);
-    bb = denoise_section<real, E>(v, bprev, bl, lane, M, c[l], tau * tau, (real)1);
+    load_section_any<real, E>(bl, bprev, lane, M);
+    bb = denoise_section<real, E>(v, bprev, bl, lane, M, c[l], tau * tau, (real)1, false);
+    store_section_any<real, E>(bl, v, lane, M);
     if (bq) {
       const double sf = bfix[0];
       int8_t* qb = bq + (long long)b * bq_ld + (long long)l * M;
-      if constexpr (E >= 4) {  // 4 consecutive elements per lane: one 4-byte store per plane
+      if (E >= 4 && (M & 3) == 0) {  // 4 consecutive elements per lane: one 4-byte store per plane
 #pragma unroll
-        for (int i = 0; i < E; i += 4) {
+        for (int i = 0; i < (E >= 4 ? E : 0); i += 4) {
           const int e = elem_index<E>(lane, i);
+          if (e >= M) continue;
           int d[4][kI8NPB];
 #pragma unroll
           for (int u = 0; u < 4; ++u) i8_digits<kI8NPB>((int)rint((double)v[i + u] * sf), d[u]);
@@ -2076,6 +2114,7 @@ enum { K_SEC = 0, K_ROW = 1, K_DAZ = 2, K_DDEN = 3, K_DAB = 4, K_QNT = 5, K_NKIN
 struct sa_ctx {
   Prof* prof = nullptr;
   int L = 0, M = 0, n = 0, w = 0, nhi = 0, backend = 0, prec = 0, device = 0;
+  bool pow2 = true;  // M a power of two (the Hadamard kernels, bit-level glue)
   int G = 0, NZ = 0, E = 1;
   int n_cus = 256;
   int Gb = 0, CB = 0;  // batched kernel: groups of kSG sections, codewords per workgroup (0 = off)
@@ -3012,7 +3051,10 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   if (backend == SA_BACKEND_DENSE && prec != SA_PREC_F32)
     return fail(SA_ERR_UNSUPPORTED, "dense backend streams an fp32 matrix (precision must be F32)");
   const bool pow2 = (M & (M - 1)) == 0;
-  if (!pow2 || M > 4096) return fail(SA_ERR_UNSUPPORTED, "M must be a power of two <= 4096");
+  if (M > 4096) return fail(SA_ERR_UNSUPPORTED, "M must be <= 4096");
+  if (!pow2 && backend == SA_BACKEND_HADAMARD)
+    return fail(SA_ERR_UNSUPPORTED, "the matrix-free Hadamard operator needs M a power of two "
+                                    "(the dense and host-operator backends take any M)");
   if (n >= 65535) return fail(SA_ERR_UNSUPPORTED, "n must be < 65535");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SA_ERR_NO_DEVICE, "no HIP device visible");
@@ -3024,7 +3066,9 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   const int mx = (M + 1) > (n + 1) ? (M + 1) : (n + 1);
   c->w = 1 << ilog2(mx);  // 2^ceil(log2(max(M+1, n+1))), sparc_ldpc.py:52/:110
   c->nhi = c->w / M;
-  c->E = M >= 64 ? M / 64 : 1;
+  c->E = 1;  // elements per lane of a one-wave section: the power of two covering M
+  while (c->E * 64 < M) c->E *= 2;
+  c->pow2 = pow2;
   if (ordering) c->ordering.assign(ordering, ordering + (size_t)L * n);
   c->NZ = (n + kRowsPerBlk - 1) / kRowsPerBlk;
   c->NZ16 = (n + kRow2Rows - 1) / kRow2Rows;
@@ -3332,6 +3376,7 @@ int check_glue(sa_ctx* c, int B, int l0, int ns) {
   if (l0 < 0 || ns <= 0 || l0 + ns > c->L) return fail(SA_ERR_ARG, "section range outside [0, L)");
   if (!c->power_set) return fail(SA_ERR_ARG, "power allocation not staged");
   if (c->M < 2) return fail(SA_ERR_UNSUPPORTED, "M < 2 carries no bits");
+  if (!c->pow2) return fail(SA_ERR_UNSUPPORTED, "bit-level glue needs M a power of two (bits2indices, sparc_ldpc.py:317)");
   if (c->M > kGlueMaxM) return fail(SA_ERR_UNSUPPORTED, "SPARC<->LDPC glue stages a section in LDS: M <= 8192");
   return SA_OK;
 }
@@ -3694,6 +3739,7 @@ int sa_encode(sa_ctx* c, int B, const int32_t* idx, const double* noise) {
   if (B <= 0 || !idx) return fail(SA_ERR_ARG, "sa_encode: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_encode: power allocation not staged");
   if (int rc0 = check_op(c, "sa_encode")) return rc0;
+  if (!c->pow2) return fail(SA_ERR_UNSUPPORTED, "sa_encode: the row-parallel encoder needs M a power of two");
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
   if (rc) return rc;
@@ -3832,6 +3878,7 @@ int sa_threshold(sa_ctx* c, int B, int l0, int ns, const double* app, int flags,
 int sa_cancel_scaled(sa_ctx* c, int B, const int32_t* idx, double scale, sa_ctx* dst) {
   if (check_ctx(c) || check_ctx(dst)) return SA_ERR_ARG;
   if (int rc0 = check_op(c, "sa_cancel")) return rc0;
+  if (!c->pow2) return fail(SA_ERR_UNSUPPORTED, "sa_cancel: needs M a power of two");
   if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_cancel: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_cancel: power allocation not staged");
   if (dst->n != c->n || dst->prec != c->prec || dst->device != c->device)

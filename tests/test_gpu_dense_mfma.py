@@ -1,9 +1,11 @@
 """GPU parity of the dense backend's batched path: Ab / Az as int8 matrix-core
 GEMMs (k_gemm_i8, sparc_ldpc_amd/csrc/dense_i8.hip) on the exact +-1 matrix
-with three-digit fixed-point vectors, for B >= 4 codewords.
+with fixed-point vectors of three (z) / four (beta) base-256 digits, for
+B >= 4 codewords; and the dense backend's section sizes that are not powers
+of two.
 
 Tolerances: the GEMM is exact for the quantised vectors; the quantisation
-error is 2^-23 of max|v_b| per element and the output is rounded to binary32,
+error is at most 2^-23 of max|v_b| per element and the output is rounded to binary32,
 so an operator product is within 1e-6 norm-relative of the fp64 oracle (per
 codeword); decodes keep the fp32 contract of the rest of the suite (1e-5
 norm-relative, identical section argmax away from near-ties).
@@ -95,3 +97,32 @@ def test_mfma_c2_batch_golden(sp):
     assert rel(bb[0], g["beta_final"]) <= 1e-5
     assert np.array_equal(orc.section_argmax(bb[0], L, M), g["argmax_final"])
     assert 0 <= it[0] <= T
+
+
+@pytest.mark.parametrize("L,M,n", [(20, 100, 300), (6, 600, 2000), (9, 48, 200)])
+def test_dense_any_section_size_vs_oracle(sp, L, M, n):
+    """M not a power of two (the reference's sub_fht takes any M,
+    sparc_ldpc.py:32-79; w = 2^ceil(log2(max(M+1, n+1)))): the dense backend's
+    fp32 GEMVs (B = 1) and int8 GEMMs (B = 6), and the decode, vs the oracle.
+    The matrix-free Hadamard backend refuses such M."""
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="dense")
+    oAb, oAz, _ = orc.sparc_transforms(L, M, n)
+    rs = np.random.RandomState(M)
+    beta = rs.randn(6, L * M)
+    z = rs.randn(6, n)
+    for B in (1, 6):
+        ab = op.Ab_batch(beta[:B])
+        az = op.Az_batch(z[:B])
+        for b in range(B):
+            assert rel(ab[b], oAb(beta[b].reshape(-1, 1))) <= 2e-6
+            assert rel(az[b], oAz(z[b].reshape(-1, 1))) <= 2e-6
+    Pl = 1.5 / L * np.ones(L)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.4, oAb, 5 + b)[1].reshape(-1) for b in range(6)])
+    for B in (1, 6):
+        bb, _ = op.amp_batch(ys[:B], Pl, 8, early_stop=False)
+        for b in range(B):
+            ref = orc._amp_core(ys[b].reshape(-1, 1), Pl, L, M, 8, oAb, oAz, None, early_stop=False)[0]
+            assert rel(bb[b], ref) <= 1e-5
+            assert np.array_equal(orc.section_argmax(bb[b], L, M), orc.section_argmax(ref, L, M))
+    with pytest.raises(sp.SparcAmpError):
+        sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="hadamard")

@@ -94,3 +94,14 @@ def test_host_context_refuses_device_operator_calls(sp):
     out = np.empty((1, 32))
     with pytest.raises(sp.SparcAmpError):
         sp._lib.check(loop._lib.sa_Az(loop._ctx, 1, sp._lib.dptr(z), sp._lib.dptr(out)))
+
+
+def test_foreign_callables_any_section_size(sp):
+    """M not a power of two through the host-operator loop (the reference's
+    operator with M = 100)."""
+    L, M, n = 12, 100, 250
+    Pl = 1.0 / L * np.ones(L)
+    oAb, oAz, _ = orc.sparc_transforms(L, M, n)
+    _, y = orc.rep_inputs(L, M, n, Pl, 0.3, oAb, 3)
+    ref = orc._amp_core(y, Pl, L, M, 10, oAb, oAz, None, early_stop=False)[0]
+    assert rel(sp.amp(y, 0, Pl, L, M, 10, oAb, oAz, early_stop=False), ref) <= 1e-11

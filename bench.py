@@ -178,6 +178,40 @@ def dense_gemv_probe(device):
     return out
 
 
+def load_sq(tag, kernel):
+    """SQ counters (mean per launch) of `kernel` from the newest committed
+    profiles/<round>_<tag>_sq_counters.txt (scripts/pmc_sq.sh), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{tag}_sq_counters.txt")))
+    if not files:
+        return None
+    out, cur = {}, None
+    for line in open(files[-1]):
+        if not line.startswith(" "):
+            cur = line.split(" ")[0]
+        elif cur == kernel:
+            k, v = line.split()
+            out[k] = float(v)
+    return (out, os.path.relpath(files[-1], ROOT)) if out else None
+
+
+def valu_bound(tag, kernel, kernel_ms, cus, clock_ghz=2.4):
+    """The batched section kernel is VALU-issue-bound, not HBM-bound: VALU
+    busy and issue fractions of the SIMDs over the kernel's duration from its
+    SQ counters (SQ_ACTIVE_INST_VALU in quad-cycles; a wave64 VALU instruction
+    issues over 2 cycles on a SIMD-32, MI355X_MICROARCH.md)."""
+    got = load_sq(tag, kernel)
+    if got is None:
+        return None
+    sq, src = got
+    simd_cycles = 4 * cus * kernel_ms * 1e-3 * clock_ghz * 1e9
+    return {"valu_busy_frac": round(4 * sq["SQ_ACTIVE_INST_VALU"] / simd_cycles, 3),
+            "valu_issue_frac": round(2 * sq["SQ_INSTS_VALU"] / simd_cycles, 3),
+            "valu_instructions_per_launch": int(sq["SQ_INSTS_VALU"]),
+            "lds_bank_conflict_cycles_frac": round(sq["SQ_LDS_BANK_CONFLICT"] / max(1.0, sq["SQ_LDS_IDX_ACTIVE"]), 3),
+            "source": src, "clock_ghz_assumed": clock_ghz}
+
+
 def load_pmc(workload, kernel):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -291,6 +325,10 @@ def main():
         "eager_decode_ms": round(total_ms, 3),
     }
 
+    if kname == "k_secb" and args.precision == "fp32":
+        vb = valu_bound(args.workload, kname, dom_ms, plan["cus"])
+        if vb is not None:
+            roofline["secondary_bound"] = dict(bound="valu", **vb)
     result = {
         "metric": f"decoded codewords/sec (T AMP iters) at L={L},M={M}; achieved HBM GB/s vs roofline",
         "value": round(B * args.steps * world / elapsed, 3),

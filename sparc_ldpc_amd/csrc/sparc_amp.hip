@@ -1226,7 +1226,10 @@ __global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real
 // workgroups of a section group are placed on one XCD (blockIdx % 8 labels
 // the XCD) so the group's tables stay in that XCD's L2.
 constexpr int kSG = 16;  // fwd table padding (sections)
-constexpr int kWB = 8;   // sections (waves) per batched workgroup
+// sections (waves) per batched workgroup: 8 (two workgroups per CU), or 16
+// (one per CU) where the wider workgroup's LDS holds a larger codeword chunk
+// (sa_ctx::WB, chosen at context creation)
+constexpr int kWB = 8, kWB16 = 16;
 
 template <typename real, int CB>
 struct cbvec;
@@ -1322,7 +1325,9 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // binary64: fewer loads in flight so a wave fits 128 VGPRs (two workgroups per CU)
   constexpr bool F64 = sizeof(real) == 8;
   constexpr int KH = (E >= 16 || CB >= 4 || F64) ? 2 : 4;  // bucket h-steps with table loads in flight together
-  constexpr int KR = (CB >= 4 || F64) ? 2 : 3;   // rows per thread whose Ab-table loads are in flight together
+  // rows per thread whose Ab-table loads are in flight together (one with 16
+  // sections at CB = 4: their 4 table words per row already fill the registers)
+  constexpr int KR = (CB >= 4 || F64) ? (W > 8 && CB >= 4 ? 1 : 2) : 3;
   constexpr bool PB = CB <= 2 && !F64;           // prefetch the previous beta with the first loads
   constexpr int W4 = W / 4;             // 4-section table groups per workgroup
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2173,7 +2178,8 @@ struct sa_ctx {
   bool pow2 = true;  // M a power of two (the Hadamard kernels, bit-level glue)
   int G = 0, NZ = 0, E = 1;
   int n_cus = 256;
-  int Gb = 0, CB = 0;  // batched kernel: groups of kSG sections, codewords per workgroup (0 = off)
+  int Gb = 0, CB = 0;  // batched kernel: groups of WB sections, codewords per workgroup (0 = off)
+  int WB = 8;          // batched kernel: sections per workgroup (kWB or kWB16)
   size_t secb_lds = 0;
   int RS = 1, KS = 1, Gd = 0;  // dense splits; Gd = dense denoiser groups
   size_t lda = 0;
@@ -2501,7 +2507,10 @@ void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.B = B;
   a.NC = (B + CB - 1) / CB;
   if (c->prof) c->prof->begin(c->stream, K_SEC);
-  PROF_REPS(c) k_secb<real, E, CB, kWB><<<c->Gb * a.NC, kWB * 64, c->secb_lds, c->stream>>>(a);
+  if (c->WB == kWB16)
+    PROF_REPS(c) k_secb<real, E, CB, kWB16><<<c->Gb * a.NC, kWB16 * 64, c->secb_lds, c->stream>>>(a);
+  else
+    PROF_REPS(c) k_secb<real, E, CB, kWB><<<c->Gb * a.NC, kWB * 64, c->secb_lds, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
 }
 
@@ -3056,9 +3065,15 @@ hipError_t lds_attr_all() {
   SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
   SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
   SA_A((k_secb<real, 8, 2, kWB>)) SA_A((k_secb<real, 16, 2, kWB>))
+  SA_A((k_secb<real, 1, 1, kWB16>)) SA_A((k_secb<real, 2, 1, kWB16>)) SA_A((k_secb<real, 4, 1, kWB16>))
+  SA_A((k_secb<real, 8, 1, kWB16>)) SA_A((k_secb<real, 16, 1, kWB16>))
+  SA_A((k_secb<real, 1, 2, kWB16>)) SA_A((k_secb<real, 2, 2, kWB16>)) SA_A((k_secb<real, 4, 2, kWB16>))
+  SA_A((k_secb<real, 8, 2, kWB16>)) SA_A((k_secb<real, 16, 2, kWB16>))
   if constexpr (sizeof(real) == 4) {
     SA_A((k_secb<real, 1, 4, kWB>)) SA_A((k_secb<real, 2, 4, kWB>)) SA_A((k_secb<real, 4, 4, kWB>))
     SA_A((k_secb<real, 8, 4, kWB>)) SA_A((k_secb<real, 16, 4, kWB>))
+    SA_A((k_secb<real, 1, 4, kWB16>)) SA_A((k_secb<real, 2, 4, kWB16>)) SA_A((k_secb<real, 4, 4, kWB16>))
+    SA_A((k_secb<real, 8, 4, kWB16>)) SA_A((k_secb<real, 16, 4, kWB16>))
   }
 #undef SA_A
   return e;
@@ -3071,7 +3086,8 @@ bool secb_no_static_lds() {
   hipFuncAttributes at;
   const void* fs[] = {(const void*)k_secb<real, 4, 1, kWB>, (const void*)k_secb<real, 8, 1, kWB>,
                       (const void*)k_secb<real, 16, 1, kWB>, (const void*)k_secb<real, 8, 2, kWB>,
-                      (const void*)k_secb<real, 16, 2, kWB>};
+                      (const void*)k_secb<real, 16, 2, kWB>, (const void*)k_secb<real, 8, 2, kWB16>,
+                      (const void*)k_secb<real, 16, 2, kWB16>, (const void*)k_secb<real, 8, 1, kWB16>};
   for (const void* f : fs)
     if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
   return true;
@@ -3138,7 +3154,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     return fail(SA_ERR_UNSUPPORTED, "section kernel does not fit in LDS (n and M too large for this precision)");
   }
   c->G = (L + kSpw - 1) / kSpw;
-  c->Gb = (L + kWB - 1) / kWB;
+  c->Gb = (L + kWB - 1) / kWB;  // (re-set after the batched width is chosen)
   if (M >= 128 && M <= 4096) {  // k_sec2: z + 2 sections' T + top-bit exchange + reductions
     const size_t need = zbytes + 2 * (size_t)M * s + 4 * (size_t)(M / 2) * s + 16 * s;
     if (need <= 160 * 1024) {
@@ -3156,16 +3172,30 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for
   // fp32 only) whose LDS image (z and T share one region) still lets two
-  // workgroups share a CU; CB = 1 takes the whole LDS if it must
-  for (int cb = (s == 4 ? 4 : 2); cb >= 1 && M <= 1024; cb >>= 1) {
-    const size_t zb = (((size_t)(n + 1) * cb * s) + 15) / 16 * 16;
-    const size_t tb = (size_t)kWB * M * cb * s;
-    const size_t need = (zb > tb ? zb : tb) + (size_t)kWB * cb * s;
-    if (need <= (cb == 1 ? 160 : 80) * 1024) {
-      c->CB = cb;
-      c->secb_lds = need;
-      break;
-    }
+  // 8-section workgroups share a CU (CB = 1 takes the whole LDS if it must);
+  // one 16-section workgroup per CU instead where its whole-LDS image holds a
+  // larger chunk (L = 768, n = 8294: CB 4 instead of 2; binary64 2 instead of
+  // 1), and in binary32 also at equal CB (half the Ab partials: the row
+  // kernel's HBM read halves, the section kernel pays a 16-wave barrier):
+  // C4 batch 256 4.45 k -> 5.51 k cw/s (binary64 2.17 k -> 2.41 k), C3
+  // 11.10 k -> 11.26 k.  SPARC_AMP_WB=8/16 forces the width.
+  {
+    auto cb_for = [&](int W) -> std::pair<int, size_t> {
+      for (int cb = (s == 4 ? 4 : 2); cb >= 1 && M <= 1024; cb >>= 1) {
+        const size_t zb = (((size_t)(n + 1) * cb * s) + 15) / 16 * 16;
+        const size_t tb = (size_t)W * M * cb * s;
+        const size_t need = (zb > tb ? zb : tb) + (size_t)W * cb * s;
+        if (need <= (cb == 1 || W > kWB ? 160 : 80) * 1024) return {cb, need};
+      }
+      return {0, 0};
+    };
+    const auto c8 = cb_for(kWB), c16 = cb_for(kWB16);
+    const char* ew = getenv("SPARC_AMP_WB");
+    const bool w16 = ew ? atoi(ew) == kWB16 : (c16.first > c8.first || (s == 4 && c16.first == c8.first));
+    c->WB = w16 && c16.first > 0 ? kWB16 : kWB;
+    c->CB = c->WB == kWB16 ? c16.first : c8.first;
+    c->secb_lds = c->WB == kWB16 ? c16.second : c8.second;
+    c->Gb = (L + c->WB - 1) / c->WB;
   }
   {
     hipDeviceProp_t prop;

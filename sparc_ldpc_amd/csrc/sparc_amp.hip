@@ -1543,62 +1543,6 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   }
   STAMP(5);
   // ---- Ab partial of the workgroup's W sections for every row ---------------
-#if SA_SECB_QUAD
-  // four consecutive rows per thread: one 16-B store of each codeword's
-  // partial, written through (sc1) so no dirty line waits for the kernel-end
-  // writeback in front of the row kernel
-  if constexpr (sizeof(real) == 4) {
-    if ((n & 3) == 0) {
-      const int nq = n >> 2;
-      for (int q0 = 0; q0 < nq; q0 += NT) {
-        const int rq = q0 + tid;
-        const int rr = rq < nq ? rq : 0;
-        real acc[CB][4];
-#pragma unroll
-        for (int c = 0; c < CB; ++c)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[c][j] = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          ushort4 fj[W4];  // row 4 rq + j's entries (loaded per row: fewer live registers)
-#pragma unroll
-          for (int q = 0; q < W4; ++q) fj[q] = fw[(size_t)q * n + 4 * (size_t)rr + j];
-#pragma unroll
-          for (int q = 0; q < W4; ++q) {
-            const uint2 w = *reinterpret_cast<const uint2*>(&fj[q]);
-            const unsigned hw[4] = {w.x, w.x >> 16, w.y, w.y >> 16};
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-              const unsigned k = __builtin_amdgcn_ubfe(hw[s4], 0, 15);
-              const real sg = (hw[s4] & 0x8000u) ? (real)-1 : (real)1;
-              real t[CB];
-              vload<real, CB>(ts + ((size_t)(q * 4 + s4) * M + k) * CB, t);
-#pragma unroll
-              for (int c = 0; c < CB; ++c) acc[c][j] = fma(t[c], sg, acc[c][j]);
-            }
-          }
-        }
-        if (rq < nq) {
-#pragma unroll
-          for (int c = 0; c < CB; ++c)
-            if (live[c]) {
-              const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-                  a.abp + ((size_t)bc[c] * a.G + g) * n, (short)0, n * 4, 0x00020000);
-              f4 v4 = {acc[c][0], acc[c][1], acc[c][2], acc[c][3]};
-              using i4v = int __attribute__((ext_vector_type(4)));
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, v4), rsrc, rq * 16, 0, SA_SECB_QUAD_AUX);
-            }
-        }
-      }
-#ifdef SA_STAMPS
-      STAMP(6);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      STAMP(7);
-#endif
-      return;
-    }
-  }
-#endif
   for (int r0 = 0; r0 < n; r0 += KR * NT) {
     ushort4 fn[KR][W4];
     const bool more = r0 + KR * NT < n;

@@ -149,13 +149,23 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
     yo[j] = Tl::XR * kI8KS + r * kI8KS;
     yz[j] = i8_swz(r);
   }
+#ifdef SA_STAMPS
+  // diagnostic build only: the in-kernel clock over the K loop of block 0
+  // (s_memtime counts shader clocks, s_memrealtime a constant 100 MHz)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    g_stamps[12] = __builtin_amdgcn_s_memtime();
+    g_stamps[13] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   for (int st = st0; st < st1; ++st) {
     const int buf = (st - st0) & 1;
     if (st + 1 < st1)
       i8_stage_load<NP>(a, smem + (buf ^ 1) * Tl::Stage, tx, ty, (long long)(st + 1) * kI8KS, wv, lane);
     const unsigned char* sb = smem + buf * Tl::Stage;
     // operand fragments double-buffered across the four 32-deep K steps:
-    // step kk + 1's LDS reads are in flight while step kk's MFMAs issue
+    // step kk + 1's LDS reads issue one between each pair of step kk's MFMAs
+    // (sched_group_barrier), so the wait before a step's MFMAs is for reads
+    // issued a whole step earlier: c3 Aβ GEMM 1.09 -> 1.03 ms
     i8v4 xf[2][NP], yf[2][2];
 #pragma unroll
     for (int kk = 0; kk <= kI8KS / 32; ++kk) {
@@ -166,9 +176,6 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) yf[kk & 1][j] = *reinterpret_cast<const i8v4*>(sb + yo[j] + ((c ^ yz[j]) << 4));
       }
-      // keep the reads above in front of the MFMAs below (the scheduler
-      // would otherwise sink them and wait for each group on the spot)
-      __builtin_amdgcn_sched_barrier(0);
       if (kk > 0) {
         const int q = (kk - 1) & 1;
 #pragma unroll
@@ -177,11 +184,28 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
           for (int j = 0; j < 2; ++j)
             acc[p][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xf[q][p], yf[q][j], acc[p][j], 0, 0, 0);
       }
+      // one next-step read between consecutive MFMAs (the step's reads were
+      // issued during the previous step's MFMAs)
+      if (kk > 0 && kk < kI8KS / 32) {
+#pragma unroll
+        for (int u = 0; u < NP + 2; ++u) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * NP - (NP + 2), 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage's DMA has landed (this wave's)
     __syncthreads();                                   // ... every wave's, and this stage is consumed
   }
 
+#ifdef SA_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    g_stamps[14] = __builtin_amdgcn_s_memtime();
+    g_stamps[15] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   // epilogue: C/D layout col = lane & 31 (matrix row y), row = (i & 3) + 8 (i >> 2) + 4 (lane >> 5)
   // (codeword); the planes of (b, y) are the same register of acc[0..NP-1]
 #pragma unroll

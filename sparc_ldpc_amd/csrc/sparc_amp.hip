@@ -137,12 +137,178 @@ __device__ __forceinline__ real xor_lane(real x) {
   }
 }
 
+// ---- binary32 cross-lane primitives with the data movement fused ---------
+// DPP move with every lane valid (row_ror / quad_perm): the compiler folds it
+// into the consuming add (v_add_f32_dpp).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+constexpr int kRor8 = 0x128, kRor4 = 0x124, kQuadX2 = 0x4E, kQuadX1 = 0xB1;
+
+// v_max_f32 without the NaN-quieting canonicalisations fmaxf carries (the
+// operands here are finite or -inf)
+__device__ __forceinline__ float max_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Sum / max over each 16-lane row, every lane of the row receiving it: the
+// xor 8 / 4 / 2 / 1 stages of wave_sum as single fused-DPP ops.  row_ror:8 is
+// lane ^ 8; after it every lane holds the same value as its lane ^ 8 partner,
+// so row_ror:4 adds the same operands as lane ^ 4 would (identical bits).
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f32<kRor8>(v);
+  v += dpp_f32<kRor4>(v);
+  v += dpp_f32<kQuadX2>(v);
+  v += dpp_f32<kQuadX1>(v);
+  return v;
+}
+// (max in inline asm: fmaxf's canonicalisations keep the compiler from fusing
+// the DPP move; each DPP op reads the previous VALU result, so two wait states
+// separate them, and the block is fenced by them on both sides)
+__device__ __forceinline__ float row_max16(float v) {
+  float r;
+  asm("s_nop 1\n\t"
+      "v_max_f32_dpp %0, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1"
+      : "=&v"(r)
+      : "v"(v));
+  return r;
+}
+
+// v_permlane{16,32}_swap of (a, b): returns {a's lower rows / half next to b's
+// lower ones, a's upper next to b's upper} (the lane placement of the ISA op)
+template <int m>
+__device__ __forceinline__ void perm_swap(float a, float b, float& lo, float& hi) {
+  static_assert(m == 16 || m == 32, "swap width");
+  const auto r = m == 16 ? __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(b), false, false)
+                         : __builtin_amdgcn_permlane32_swap(__float_as_int(a), __float_as_int(b), false, false);
+  lo = __int_as_float((int)r[0]);
+  hi = __int_as_float((int)r[1]);
+}
+// The xor 32 (16) reduction stage of two values at once: lanes 0-31 (rows
+// 0, 2) receive a's lower + upper halves (rows), lanes 32-63 (rows 1, 3) b's
+template <int m, bool MAX>
+__device__ __forceinline__ float swap_op(float a, float b) {
+  float lo, hi;
+  perm_swap<m>(a, b, lo, hi);
+  return MAX ? max_raw(lo, hi) : lo + hi;
+}
+__device__ __forceinline__ float readlane_f32(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Reductions of CB per-codeword wave values together (binary32): codeword
+// pairs share the permlane32 stage (one per 32-lane half), pairs of those the
+// permlane16 stage (one codeword per 16-lane row: 0, 2, 1, 3), then one row
+// reduction serves all; the same operand pairs in the same order as
+// wave_sum / wave_max per codeword, so the same bits.  Results are uniform.
+template <bool MAX, int CB>
+__device__ __forceinline__ void wave_reduce_cb(float (&v)[CB]) {
+  static_assert(CB == 1 || CB == 2 || CB == 4, "codewords per reduction");
+  if constexpr (CB == 1) {
+    float p = swap_op<32, MAX>(v[0], v[0]);
+    p = swap_op<16, MAX>(p, p);
+    v[0] = readlane_f32(MAX ? row_max16(p) : row_sum16(p), 0);
+  } else if constexpr (CB == 2) {
+    float p = swap_op<32, MAX>(v[0], v[1]);
+    p = swap_op<16, MAX>(p, p);
+    p = MAX ? row_max16(p) : row_sum16(p);
+    v[0] = readlane_f32(p, 0);
+    v[1] = readlane_f32(p, 32);
+  } else {
+    const float p01 = swap_op<32, MAX>(v[0], v[1]);
+    const float p23 = swap_op<32, MAX>(v[2], v[3]);
+    float q = swap_op<16, MAX>(p01, p23);
+    q = MAX ? row_max16(q) : row_sum16(q);
+    v[0] = readlane_f32(q, 0);
+    v[2] = readlane_f32(q, 16);
+    v[1] = readlane_f32(q, 32);
+    v[3] = readlane_f32(q, 48);
+  }
+}
+// Butterfly on lane bit 4 or 8 (binary32): the lower banks of each row take
+// x + x[lane + m], the upper ones x[lane - m] - x, each as one bank-masked
+// DPP add / sub (two VALU ops per element instead of two moves and an fma;
+// the same two operands and rounding).  Two wait states fence the block.
+template <int m, int E>
+__device__ __forceinline__ void bfly_bank_f32(float (&x)[E]) {
+  static_assert(m == 4 || m == 8, "bank butterfly");
+  static_assert(E == 1 || E % 2 == 0, "pairs");
+#pragma unroll
+  for (int i = 0; i < E; i += 2) {
+    float r0, r1;
+    if constexpr (E == 1) {
+      if constexpr (m == 4)
+        asm("s_nop 1\n\t"
+            "v_add_f32_dpp %0, %1, %1 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+            "v_sub_f32_dpp %0, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+            "s_nop 1"
+            : "=&v"(r0) : "v"(x[i]));
+      else
+        asm("s_nop 1\n\t"
+            "v_add_f32_dpp %0, %1, %1 row_shl:8 row_mask:0xf bank_mask:0x3\n\t"
+            "v_sub_f32_dpp %0, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+            "s_nop 1"
+            : "=&v"(r0) : "v"(x[i]));
+      x[i] = r0;
+    } else {
+      if constexpr (m == 4)
+        asm("s_nop 1\n\t"
+            "v_add_f32_dpp %0, %2, %2 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+            "v_add_f32_dpp %1, %3, %3 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+            "v_sub_f32_dpp %0, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+            "v_sub_f32_dpp %1, %3, %3 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+            "s_nop 1"
+            : "=&v"(r0), "=&v"(r1) : "v"(x[i]), "v"(x[i + 1]));
+      else
+        asm("s_nop 1\n\t"
+            "v_add_f32_dpp %0, %2, %2 row_shl:8 row_mask:0xf bank_mask:0x3\n\t"
+            "v_add_f32_dpp %1, %3, %3 row_shl:8 row_mask:0xf bank_mask:0x3\n\t"
+            "v_sub_f32_dpp %0, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+            "v_sub_f32_dpp %1, %3, %3 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+            "s_nop 1"
+            : "=&v"(r0), "=&v"(r1) : "v"(x[i]), "v"(x[i + 1]));
+      x[i] = r0;
+      x[i + 1] = r1;
+    }
+  }
+}
+
+// Butterfly on lane bit 16 or 32 (binary32) for two elements at once: one
+// permlane swap puts both elements' lower halves (rows) in one register and
+// their upper ones in another, an add and a sub form the outputs, a second
+// swap puts them back in place: four VALU ops per two elements instead of six
+// (lower lanes a + b, upper a - b, as before).
+template <int m, int E>
+__device__ __forceinline__ void bfly_swap_f32(float (&x)[E]) {
+  static_assert(E % 2 == 0, "pairs");
+#pragma unroll
+  for (int i = 0; i < E; i += 2) {
+    float a, b;
+    perm_swap<m>(x[i], x[i + 1], a, b);
+    perm_swap<m>(a + b, a - b, x[i], x[i + 1]);
+  }
+}
+
 // One lane-bit butterfly stage: lower lane x + p, upper lane p - x, as a
 // single fma with the per-lane sign (+1 lower, -1 upper).
 template <int m, typename real, int E>
 __device__ __forceinline__ void lane_butterfly(real (&x)[E], int lane) {
   const real sg = (lane & m) ? (real)-1 : (real)1;
-  if constexpr ((m == 16 || m == 32) && sizeof(real) == 4) {
+  if constexpr ((m == 4 || m == 8) && sizeof(real) == 4) {
+    bfly_bank_f32<m, E>(x);
+  } else if constexpr ((m == 16 || m == 32) && sizeof(real) == 4 && E % 2 == 0) {
+    bfly_swap_f32<m, E>(x);
+  } else if constexpr ((m == 16 || m == 32) && sizeof(real) == 4) {
     // v_permlane{16,32}_swap of x with itself leaves a = the lower partner
     // and b = the upper one in every lane: lower lanes a + b, upper a - b
     // (the same two operands and rounding as fma(x, sg, partner))
@@ -165,6 +331,11 @@ __device__ __forceinline__ void lane_butterfly(real (&x)[E], int lane) {
 // Full-wave xor-butterfly reductions (fixed order: deterministic bits).
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
+  if constexpr (sizeof(T) == 4 && (T)0.5 != 0) {  // binary32: fused stages, same pairs
+    v = swap_op<32, false>(v, v);
+    v = swap_op<16, false>(v, v);
+    return row_sum16(v);
+  }
   v += xor_lane<32>(v);
   v += xor_lane<16>(v);
   v += xor_lane<8>(v);
@@ -176,6 +347,13 @@ __device__ __forceinline__ T wave_sum(T v) {
 
 template <typename T>
 __device__ __forceinline__ void wave_sum2(T& a, T& b) {
+  if constexpr (sizeof(T) == 4 && (T)0.5 != 0) {  // binary32: both in one register after xor 32
+    float v[2] = {a, b};
+    wave_reduce_cb<false, 2>(v);
+    a = v[0];
+    b = v[1];
+    return;
+  }
   a += xor_lane<32>(a); b += xor_lane<32>(b);
   a += xor_lane<16>(a); b += xor_lane<16>(b);
   a += xor_lane<8>(a); b += xor_lane<8>(b);
@@ -186,6 +364,11 @@ __device__ __forceinline__ void wave_sum2(T& a, T& b) {
 
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
+  if constexpr (sizeof(T) == 4 && (T)0.5 != 0) {  // binary32
+    float r[1] = {v};
+    wave_reduce_cb<true, 1>(r);
+    return r[0];
+  }
   T o;
   o = xor_lane<32>(v); v = o > v ? o : v;
   o = xor_lane<16>(v); v = o > v ? o : v;
@@ -194,6 +377,11 @@ __device__ __forceinline__ T wave_max(T v) {
   o = xor_lane<2>(v); v = o > v ? o : v;
   o = xor_lane<1>(v); v = o > v ? o : v;
   return v;
+}
+template <bool MAX, int CB>
+__device__ __forceinline__ void wave_reduce_cb(double (&v)[CB]) {
+#pragma unroll
+  for (int c = 0; c < CB; ++c) v[c] = MAX ? wave_max(v[c]) : wave_sum(v[c]);
 }
 
 // In-wave natural-order Walsh-Hadamard transform of one section.
@@ -700,7 +888,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
       }
     }
   STAMP(3);
-    fwht_wave<real, E>(v, lane, mlanes);
+    fwht_wave<real, E>(v, lane, E >= 2 ? 64 : mlanes);  // E >= 2: M = 64 E, every lane
   STAMP(4);
     if (a.mode == SEC_AZ) {
       if (have && owner) {
@@ -718,7 +906,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     }
   }
   if (have) {
-    fwht_wave<real, E>(v, lane, mlanes);  // T_l = H_M beta_l
+    fwht_wave<real, E>(v, lane, E >= 2 ? 64 : mlanes);  // T_l = H_M beta_l
   STAMP(6);
   } else {
 #pragma unroll
@@ -1497,19 +1685,52 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     }
   }
   STAMP(3);
-  real bbl[CB];
+  // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
+  // codewords with their section max / sums reduced together (wave_reduce_cb)
+  const int ml = E >= 2 ? 64 : mlanes;  // E >= 2: M = 64 E fills every lane
+  const real inv_sn = (real)1 / a.sqrt_n;
+  real bbl[CB], mx[CB], S[CB], S2[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     if constexpr (!PB) {
       if (c + 1 < CB)
         load_section<real, E>(a.beta + (size_t)bc[c + 1] * LM + (size_t)lc * M, bprev[(c + 1) & 1], lane, M);
     }
-    fwht_wave<real, E>(v[c], lane, mlanes);
-    real* bl = a.beta + (size_t)bc[c] * LM + (size_t)lc * M;
-    bbl[c] = denoise_section<real, E>(v[c], bprev[PB ? c : (c & 1)], bl, lane, M, cl[c], tau2[c], a.sqrt_n,
-                                      have && live[c]);
+    fwht_wave<real, E>(v[c], lane, ml);
+    const real k = cl[c] / tau2[c];
+    real m = neg_inf<real>();
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const real u = fma(v[c][i], inv_sn, bprev[PB ? c : (c & 1)][i]) * k;  // :213, :215
+      v[c][i] = (E >= 2 || elem_index<E>(lane, i) < M) ? u : neg_inf<real>();
+      m = v[c][i] > m ? v[c][i] : m;
+    }
+    mx[c] = m;
+  }
+  wave_reduce_cb<true, CB>(mx);  // :216 (per section)
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    real s = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      v[c][i] = dexp<real>(v[c][i] - mx[c]);  // :217; exp(-inf) = 0 on idle lanes
+      s += v[c][i];
+      s2 += v[c][i] * v[c][i];
+    }
+    S[c] = s;
+    S2[c] = s2;
+  }
+  wave_reduce_cb<false, CB>(S);   // :218
+  wave_reduce_cb<false, CB>(S2);  // sum(beta^2)
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const real scale = cl[c] / S[c];  // :219
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[c][i] *= scale;
+    if (have && live[c]) store_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, v[c], lane, M);
     if (have) {
-      fwht_wave<real, E>(v[c], lane, mlanes);  // T_l = H_M beta_l
+      bbl[c] = S2[c] * scale * scale;
+      fwht_wave<real, E>(v[c], lane, ml);  // T_l = H_M beta_l
     } else {
       bbl[c] = 0;
 #pragma unroll

@@ -80,6 +80,13 @@ __device__ __forceinline__ T ld_vmem(const T* p) {
 // Store of a partial another kernel reads after the boundary (Ab partials):
 // non-temporal, so no dirty L2 line is left for the kernel-end writeback to
 // drain (c2: k_sec4 7.85 -> 7.65 us, +1.5 % codewords/s; c3 neutral).
+// load at a uniform base + 32-bit byte offset (SGPR-base addressing, no
+// 64-bit address arithmetic per load)
+template <typename T>
+__device__ __forceinline__ T ld_off(const T* base, unsigned byte_off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 template <typename T>
 __device__ __forceinline__ void st_part(T* p, T v) {
   __builtin_nontemporal_store(v, p);
@@ -406,6 +413,45 @@ __device__ __forceinline__ void fwht_wave(real (&x)[E], int lane, int mlanes) {
   if (mlanes > 8) lane_butterfly<8>(x, lane);
   if (mlanes > 16) lane_butterfly<16>(x, lane);
   if (mlanes > 32) lane_butterfly<32>(x, lane);
+}
+
+// The same transform (binary32, E >= 2, all 64 lanes) with the lane-bit 0 / 1
+// butterflies as single in-place DPP fmas x += s * x[lane ^ m] (s = +1 in the
+// lower lane, -1 in the upper): the upper lane then holds b - a = -(a - b),
+// exactly (rounding is sign-symmetric), and the later stages pair lanes of
+// equal sign, so lane L ends with (-1)^(L0 + L1) times the value fwht_wave
+// leaves there.  s1 / s2 are the per-lane signs of lane bits 0 / 1.  The
+// caller cancels the sign (k_secb: input signs, quad-mirrored section
+// positions and a signed 1/sqrt(n); see there).
+template <int E>
+__device__ __forceinline__ void fwht_wave_sgn(float (&x)[E], float s1, float s2) {
+  static_assert(E >= 2 && E % 2 == 0, "pairs of elements");
+#pragma unroll
+  for (int h = 1; h < E; h <<= 1) {
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (!(i & h)) {
+        const float a = x[i], b = x[i | h];
+        x[i] = a + b;
+        x[i | h] = a - b;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < E; i += 2)
+    asm("s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %0, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %0, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %1, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1"
+        : "+v"(x[i]), "+v"(x[i + 1])
+        : "v"(s1), "v"(s2));
+  bfly_bank_f32<4, E>(x);
+  bfly_bank_f32<8, E>(x);
+  bfly_swap_f32<16, E>(x);
+  bfly_swap_f32<32, E>(x);
 }
 
 template <typename real> __device__ __forceinline__ real dsqrt(real x);
@@ -1522,6 +1568,20 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   const int M = a.M, n = a.n;
   const size_t LM = (size_t)a.L * M;
   const int mlanes = M < 64 ? M : 64;
+  // SGN (binary32, E >= 2): both transforms run fwht_wave_sgn, which leaves
+  // slot k (lane L) with (-1)^<k,m> = sgl times the transform, m the two
+  // index bits on lane bits 0 / 1.  Cancelled exactly with no table change:
+  // the bucket gather and beta use quad-mirrored section positions (lane L
+  // holds index k ^ m: lane L ^ 3's) and the gathered input is multiplied by
+  // sgl.  With H(x(. ^ m))[k] = (-1)^<k,m> (Hx)[k] the first transform then
+  // yields Az at the mirrored positions with no sign (the denoiser and beta
+  // stay in that layout) and the second, fed mirrored beta, T = H beta in
+  // natural positions with no sign: the same values, bit for bit, as
+  // fwht_wave on the natural layout.
+  constexpr bool SGN = sizeof(real) == 4 && E >= 2;
+  const int lpos = SGN ? (lane ^ 3) : lane;  // section positions of this lane
+  const real sgl = (SGN && (__popc(lane & 3) & 1)) ? (real)-1 : (real)1;
+  const float s1 = (lane & 1) ? -1.f : 1.f, s2 = (lane & 2) ? -1.f : 1.f;
   STAMP(0);
 
   // XCD-grouped work mapping (speed only: any placement is correct)
@@ -1574,24 +1634,28 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // z rows of the CB codewords (first pass of the staging loop)
   constexpr int KZ = 4;
   real zr[KZ][CB];
+  // uniform codeword bases + 32-bit unsigned row offsets (SGPR-base loads)
+  const real* zc[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) zc[c] = a.z + (size_t)bc[c] * n;
 #pragma unroll
   for (int u = 0; u < KZ; ++u) {
     const int r = u * NT + tid;
 #pragma unroll
-    for (int c = 0; c < CB; ++c) zr[u][c] = a.z[(size_t)bc[c] * n + (r < n ? r : 0)];
+    for (int c = 0; c < CB; ++c) zr[u][c] = ld_off(zc[c], (unsigned)(r < n ? r : 0) * (unsigned)sizeof(real));
   }
   const uint16_t* il = a.inv + (size_t)lc * a.w;
   ushort4 tb[KH][NQ];
-  load_buckets<E, KH>(il, 0, a.nhi, M, lane, tb);
+  load_buckets<E, KH>(il, 0, a.nhi, M, lpos, tb);
   // previous beta: all CB codewords up front when registers allow (CB <= 2),
   // else codeword 0 now and codeword c+1 while c is denoised (PB false)
   real bprev[PB ? CB : 2][E];
   if constexpr (PB) {
 #pragma unroll
     for (int c = 0; c < CB; ++c)
-      load_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lane, M);
+      load_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lpos, M);
   } else {
-    load_section<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lane, M);
+    load_section<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lpos, M);
   }
   real cl[CB];
 #pragma unroll
@@ -1636,7 +1700,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       for (int u = 0; u < KZ; ++u) {
         const int r = r0 + KZ * NT + u * NT + tid;
 #pragma unroll
-        for (int c = 0; c < CB; ++c) zr[u][c] = a.z[(size_t)bc[c] * n + (r < n ? r : 0)];
+        for (int c = 0; c < CB; ++c) zr[u][c] = ld_off(zc[c], (unsigned)(r < n ? r : 0) * (unsigned)sizeof(real));
       }
     }
   }
@@ -1655,12 +1719,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     for (int h0 = 0; h0 < a.nhi; h0 += KH) {
       ushort4 tn[KH][NQ];
       const bool more = h0 + KH < a.nhi;
-      if (more) load_buckets<E, KH>(il, h0 + KH, a.nhi, M, lane, tn);
+      if (more) load_buckets<E, KH>(il, h0 + KH, a.nhi, M, lpos, tn);
 #pragma unroll
       for (int hh = 0; hh < KH; ++hh) {
         if (h0 + hh < a.nhi) {
           // sgn(h): the high index bits of w-M+c are all ones
-          const real sg = (__popc(h0 + hh) & 1) ? (real)-1 : (real)1;
+          const real sg = (__popc(h0 + hh) & 1) ? -sgl : sgl;
           if constexpr (E >= 4) {
             gather_step4<real, E, CB>(reinterpret_cast<const unsigned char*>(zs), tb[hh], sg, v);
           } else {
@@ -1688,20 +1752,27 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
   // codewords with their section max / sums reduced together (wave_reduce_cb)
   const int ml = E >= 2 ? 64 : mlanes;  // E >= 2: M = 64 E fills every lane
+  auto fwht_sec = [&](real (&x)[E]) {
+    if constexpr (SGN) fwht_wave_sgn<E>(x, s1, s2);
+    else fwht_wave<real, E>(x, lane, ml);
+  };
   const real inv_sn = (real)1 / a.sqrt_n;
   real bbl[CB], mx[CB], S[CB], S2[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     if constexpr (!PB) {
       if (c + 1 < CB)
-        load_section<real, E>(a.beta + (size_t)bc[c + 1] * LM + (size_t)lc * M, bprev[(c + 1) & 1], lane, M);
+        load_section<real, E>(a.beta + (size_t)bc[c + 1] * LM + (size_t)lc * M, bprev[(c + 1) & 1], lpos, M);
     }
-    fwht_wave<real, E>(v[c], lane, ml);
+    fwht_sec(v[c]);
     const real k = cl[c] / tau2[c];
     real m = neg_inf<real>();
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      const real u = fma(v[c][i], inv_sn, bprev[PB ? c : (c & 1)][i]) * k;  // :213, :215
+      // :213, :215.  The exponent argument below, u - max, is contracted to
+      // fma(s, k, -max) (one rounding where the reference rounds u first:
+      // <= 1 ulp of u, inside the parity bounds; 4 % faster at c3)
+      const real u = fma(v[c][i], inv_sn, bprev[PB ? c : (c & 1)][i]) * k;
       v[c][i] = (E >= 2 || elem_index<E>(lane, i) < M) ? u : neg_inf<real>();
       m = v[c][i] > m ? v[c][i] : m;
     }
@@ -1727,10 +1798,10 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     const real scale = cl[c] / S[c];  // :219
 #pragma unroll
     for (int i = 0; i < E; ++i) v[c][i] *= scale;
-    if (have && live[c]) store_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, v[c], lane, M);
+    if (have && live[c]) store_section<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, v[c], lpos, M);
     if (have) {
       bbl[c] = S2[c] * scale * scale;
-      fwht_wave<real, E>(v[c], lane, ml);  // T_l = H_M beta_l
+      fwht_sec(v[c]);  // T_l = H_M beta_l (natural positions)
     } else {
       bbl[c] = 0;
 #pragma unroll
@@ -1764,6 +1835,8 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   }
   STAMP(5);
   // ---- Ab partial of the workgroup's W sections for every row ---------------
+  constexpr int SHB = ilog2c<CB * (int)sizeof(real)>();      // T element k -> byte k << SHB
+  const unsigned secb = (unsigned)M * CB * (unsigned)sizeof(real);  // bytes per staged section
   for (int r0 = 0; r0 < n; r0 += KR * NT) {
     ushort4 fn[KR][W4];
     const bool more = r0 + KR * NT < n;
@@ -1784,14 +1857,31 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
 #pragma unroll
       for (int q = 0; q < W4; ++q) {
         const uint2 w = *reinterpret_cast<const uint2*>(&f[u][q]);
-        const unsigned hw[4] = {w.x, w.x >> 16, w.y, w.y >> 16};
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
           // entry = k | sign << 15: T element k of section q*4+s4, sign -> +-1.0
-          const unsigned k = __builtin_amdgcn_ubfe(hw[s4], 0, 15);
-          const real sg = (hw[s4] & 0x8000u) ? (real)-1 : (real)1;
+          const unsigned wd = s4 < 2 ? w.x : w.y;
+          const bool up = s4 & 1;
           real t[CB];
-          vload<real, CB>(ts + ((size_t)(q * 4 + s4) * M + k) * CB, t);
+          real sg;
+          if constexpr (sizeof(real) == 4) {
+            // binary32: k and the LDS byte address in two ops, the sign
+            // bit ORed into 1.0f (one op for the upper half-word)
+            const unsigned k = up ? __builtin_amdgcn_ubfe(wd, 16, 15) : (wd & 0x7fffu);
+            const unsigned sb = (up ? wd : wd << 16) & 0x80000000u;
+            sg = __uint_as_float(sb | 0x3f800000u);
+            using V = real __attribute__((ext_vector_type(CB)));
+            using lds_v = __attribute__((address_space(3))) const V;
+            // ts is LDS address 0 (the dynamic region, no static LDS)
+            const V x = *reinterpret_cast<lds_v*>((size_t)((k << SHB) + (unsigned)(q * 4 + s4) * secb));
+#pragma unroll
+            for (int c = 0; c < CB; ++c) t[c] = x[c];
+          } else {
+            const unsigned hw = up ? wd >> 16 : wd;
+            const unsigned k = __builtin_amdgcn_ubfe(hw, 0, 15);
+            sg = (hw & 0x8000u) ? (real)-1 : (real)1;
+            vload<real, CB>(ts + ((size_t)(q * 4 + s4) * M + k) * CB, t);
+          }
 #pragma unroll
           for (int c = 0; c < CB; ++c) acc[c] = fma(t[c], sg, acc[c]);
         }

@@ -2004,6 +2004,89 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   if (lane == 0) a.zzp[(size_t)b * a.NZ + blockIdx.x] = s;
 }
 
+// k_row with V-float accesses (binary32, n % V == 0, many codewords; V = 4:
+// 16 bytes, 256 rows per workgroup; V = 2: 8 bytes, 128 rows): V rows per
+// lane, so each load instruction of the partial stream moves 64 V floats per
+// wave (k_row: 64).  Per row the same sums as k_row in the same order (wave w
+// adds its partial range in order, the four wave sums are added in wave
+// order); the z^2 partials cover 64 V rows.
+template <int V>
+__global__ void __launch_bounds__(256) k_rowv(RowArgs<float> a) {
+  using fv = float __attribute__((ext_vector_type(V)));
+  __shared__ fv red[4][64];
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = a.n;
+  const int r = blockIdx.x * 64 * V + lane * V;  // the lane's first row
+  const bool in = r < n;                          // n % V == 0: V rows or none
+  float tau = 1, last = 0;
+  if (a.mode == ROW_AMP) {
+    tau = ld_vmem(a.tau + (size_t)b * a.T1 + a.t);
+    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : 0.f;
+  }
+  const size_t o = (size_t)b * n + (in ? r : 0);
+  fv yv = {}, zv = {};
+  float bbv[2] = {0.f, 0.f};
+  if (wv == 0) {
+    yv = *reinterpret_cast<const fv*>(a.y + o);
+    if (a.mode == ROW_AMP) {
+      zv = *reinterpret_cast<const fv*>(a.z + o);
+      const float* bp = a.bbp + (size_t)b * a.Gb;
+      bbv[0] = lane < a.Gb ? bp[lane] : 0.f;
+      bbv[1] = lane + 64 < a.Gb ? bp[lane + 64] : 0.f;
+    }
+  }
+  if (a.mode != ROW_INIT0) {
+    const int gq = (a.G + 3) / 4;
+    const int g0 = wv * gq, g1 = min(a.G, g0 + gq);
+    const float* p = a.abp + (size_t)b * a.G * n + (in ? r : 0);
+    fv acc = {};
+    constexpr int U = 8;
+    for (int gg = g0; gg < g1; gg += U) {
+      fv t[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)  // the partials are dead after this read: streaming loads
+        t[u] = __builtin_nontemporal_load(reinterpret_cast<const fv*>(p + (size_t)(gg + u < g1 ? gg + u : g0) * n));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (gg + u < g1) acc += t[u];
+    }
+    red[wv][lane] = acc;
+  }
+  if (a.mode == ROW_AMP && a.early_stop && tau == last) return;  // uniform over the workgroup
+  const float tau2 = tau * tau;
+  __syncthreads();
+  if (wv != 0) return;
+  float ons = 0;
+  if (a.mode == ROW_AMP) {
+    const float bb = a.Gb <= 128 ? wave_sum_pair(bbv[0], bbv[1]) : wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
+    ons = a.Pb[(size_t)b * a.Pbst] - bb / (float)n;
+  }
+  fv zn = {};
+  if (in) {
+    if (a.mode == ROW_INIT0) {
+      zn = yv;
+    } else {
+      fv sv = {};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) sv += red[w][lane];
+      const fv ab = sv / a.sqrt_n;
+      if (a.mode == ROW_ABOUT) {
+        *reinterpret_cast<fv*>(a.out + o) = ab;
+        return;
+      }
+      zn = yv - ab;
+      if (a.mode == ROW_AMP) zn += (zv / tau2) * ons;
+    }
+    *reinterpret_cast<fv*>(a.z + o) = zn;
+  }
+  if (a.mode == ROW_ABOUT) return;
+  float q = 0;
+#pragma unroll
+  for (int j = 0; j < V; ++j) q += zn[j] * zn[j];
+  const float s = wave_sum(q);
+  if (lane == 0) a.zzp[(size_t)b * a.NZ + blockIdx.x] = s;
+}
+
 // Row kernel for small batches: 32 rows per 512-thread workgroup, so the
 // ceil(n/32) workgroups of a codeword spread over twice as many CUs as
 // k_row's 64-row workgroups.  Thread (row rl, group pg) sums the Ab
@@ -2447,6 +2530,8 @@ struct sa_ctx {
   bool sec4 = false;   // k_sec4 (4 waves per section) fits and is chosen
   size_t sec4_lds = 0;
   int NZ16 = 0;        // k_row2 16-row blocks; nz_cur = z^2 partial count of the current decode
+  int NZ4 = 0, NZ2 = 0;  // k_rowv<4> 256-row / k_rowv<2> 128-row blocks
+  int row_kind = 0;    // row kernel of the current decode: 0 k_row, 1 k_row2, 2 k_rowv<4>, 3 k_rowv<2>
   int nz_cur = 0;
   size_t sec2_lds = 0;
   std::vector<uint32_t> ordering;
@@ -2877,16 +2962,43 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
   return SA_OK;
 }
 
+// Row kernel for B codewords: k_row2 (32-row blocks) while B * ceil(n/64) <
+// 4 CUs, else in binary32 k_rowv<4> (n % 4 == 0) or k_rowv<2> (n even) when
+// their blocks cover the CUs twice, else k_row (64 rows).
+int row_kind_for(const sa_ctx* c, int B) {
+  if ((long long)B * c->NZ < 4LL * c->n_cus) return 1;
+  if (c->prec == SA_PREC_F32 && c->n % 4 == 0 && (long long)B * c->NZ4 >= 2LL * c->n_cus) return 2;
+  if (c->prec == SA_PREC_F32 && c->n % 2 == 0 && (long long)B * c->NZ2 >= 2LL * c->n_cus) return 3;
+  return 0;
+}
+int nz_for(const sa_ctx* c, int kind) {
+  return kind == 1 ? c->NZ16 : (kind == 2 ? c->NZ4 : (kind == 3 ? c->NZ2 : c->NZ));
+}
+void pick_row(sa_ctx* c, int B) {
+  c->row_kind = row_kind_for(c, B);
+  c->nz_cur = nz_for(c, c->row_kind);  // z^2 partials per codeword
+}
+
 template <typename real>
 int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb) {
   RowArgs<real> a = row_args<real>(c, mode, t, es, G, Gb);
   if (c->prof) c->prof->begin(c->stream, K_ROW);
   // small batch: 16-row workgroups cover the chip; many codewords: 64-row
   // workgroups, 4 waves with deeper per-lane load streams
-  if (c->nz_cur == c->NZ16)
+  if (c->row_kind == 1) {
     PROF_REPS(c) k_row2<real><<<dim3(c->NZ16, B), 16 * kRow2Rows, 0, c->stream>>>(a);
-  else
+  } else if (c->row_kind >= 2) {
+    if constexpr (sizeof(real) == 4) {
+      if (c->row_kind == 2)
+        PROF_REPS(c) k_rowv<4><<<dim3(c->NZ4, B), 256, 0, c->stream>>>(a);
+      else
+        PROF_REPS(c) k_rowv<2><<<dim3(c->NZ2, B), 256, 0, c->stream>>>(a);
+    } else {
+      return SA_ERR_UNSUPPORTED;  // never chosen for binary64 (row_kind_for)
+    }
+  } else {
     PROF_REPS(c) k_row<real, 4><<<dim3(c->NZ, B), 4 * 64, 0, c->stream>>>(a);
+  }
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -3059,7 +3171,7 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const int S8 = i8 ? i8_splits(c, B) : 0;
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
-  c->nz_cur = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;  // z^2 partials: k_row2 or k_row blocks
+  pick_row(c, B);  // row kernel and its z^2 partial count
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
   const int G = i8 ? S8 : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
@@ -3399,6 +3511,8 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   if (ordering) c->ordering.assign(ordering, ordering + (size_t)L * n);
   c->NZ = (n + kRowsPerBlk - 1) / kRowsPerBlk;
   c->NZ16 = (n + kRow2Rows - 1) / kRow2Rows;
+  c->NZ4 = (n + 255) / 256;
+  c->NZ2 = (n + 127) / 128;
   c->nz_cur = c->NZ;
   // section kernel LDS: z slots + 4 sections x M + 4 beta^2 partials
   const size_t s = rsz(c);
@@ -3911,7 +4025,7 @@ int check_host(sa_ctx* c, int B, const char* what) {
 template <typename real>
 int host_init_impl(sa_ctx* c, int B, const double* beta0, const double* ab0) {
   int rc;
-  c->nz_cur = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;
+  pick_row(c, B);
   k_fill32<<<(B + 255) / 256, 256, 0, c->stream>>>((uint32_t*)c->d_iters, 0xffffffffu, (size_t)B);
   if (beta0) {  // z = y - Ab(beta0) with the caller's Ab(beta0) (sparc_ldpc.py:196-200)
     if ((rc = upload(c, c->d_beta, beta0, (size_t)B * c->L * c->M))) return rc;
@@ -4251,9 +4365,9 @@ int sa_plan(sa_ctx* c, int B, int64_t* o) {
   o[1] = i8 ? i8_splits(c, B) : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
   o[3] = batched ? c->CB : 1;
-  o[4] = B * c->NZ < 4 * c->n_cus ? c->NZ16 : c->NZ;
+  o[4] = nz_for(c, row_kind_for(c, B));
   o[5] = c->w;
-  o[6] = B * c->NZ < 4 * c->n_cus ? 1 : 0;
+  o[6] = row_kind_for(c, B);
   o[7] = c->n_cus;
   return SA_OK;
 }

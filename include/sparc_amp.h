@@ -213,7 +213,7 @@ int sa_host_residual(sa_ctx* ctx, int B, int t, int flags, const double* ab);
  * 1 k_sec2, 2 k_secb, 3 dense fp32 GEMVs, 4 k_sec4, 5 k_sec43, 6 dense int8
  * MFMA GEMMs), Ab partials per codeword, row splits,
  * codewords per batched workgroup, z^2 partials, w, row kernel (1 k_row2,
- * 2 k_rowv<4>, 3 k_rowv<2>, 0 k_row), number of CUs}. */
+ * 2 k_rowv 16-byte rows, 3 k_rowv 8-byte rows, 0 k_row), number of CUs}. */
 int sa_plan(sa_ctx* ctx, int B, int64_t* out8);
 int sa_info(const sa_ctx* ctx, int64_t* out8); /* L, M, n, w, backend, precision, device, bytes */
 int sa_device_count(void);

@@ -112,16 +112,19 @@ __device__ __forceinline__ int elem_index(int lane, int i) {
 template <int m>
 __device__ __forceinline__ int xor_lane_i32(int x) {
   if constexpr (m == 1) {
-    return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
   } else if constexpr (m == 2) {
-    return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  } else if constexpr (m == 4 || m == 8) {
-    // two bank-masked DPP moves, no select: the banks (4-lane groups of a
-    // 16-lane row) whose lane bit m is set take row_shr:m (lane - m), the
-    // others row_shl:m (lane + m); every source lane stays inside its row
-    constexpr int hi = m == 4 ? 0xA : 0xC, lo = m == 4 ? 0x5 : 0x3;
-    const int dn = __builtin_amdgcn_update_dpp(x, x, 0x110 + m, 0xF, hi, false);
-    return __builtin_amdgcn_update_dpp(dn, x, 0x100 + m, 0xF, lo, false);
+    return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+  } else if constexpr (m == 8) {
+    return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true);  // row_ror:8 = lane ^ 8
+  } else if constexpr (m == 4) {
+    // two bank-masked DPP moves into one register, no copy and no select:
+    // the banks (4-lane groups of a 16-lane row) whose lane bit 2 is set take
+    // row_shr:4 (lane - 4), the others row_shl:4 (lane + 4), every source lane
+    // inside its row (the first move leaves the other banks undefined, the
+    // second fills them)
+    const int dn = __builtin_amdgcn_mov_dpp(x, 0x114, 0xF, 0xA, false);
+    return __builtin_amdgcn_update_dpp(dn, x, 0x104, 0xF, 0x5, false);
   } else if constexpr (m == 16) {
     const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
     return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
@@ -201,16 +204,59 @@ __device__ __forceinline__ void perm_swap(float a, float b, float& lo, float& hi
   lo = __int_as_float((int)r[0]);
   hi = __int_as_float((int)r[1]);
 }
+// binary64 values cross lanes as two 32-bit halves
+__device__ __forceinline__ int dlo(double x) { return (int)(__double_as_longlong(x) & 0xffffffffLL); }
+__device__ __forceinline__ int dhi(double x) { return (int)(__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ double djoin(int lo, int hi) {
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int m>
+__device__ __forceinline__ void perm_swap(double a, double b, double& lo, double& hi) {
+  float l0, h0, l1, h1;
+  perm_swap<m>(__int_as_float(dlo(a)), __int_as_float(dlo(b)), l0, h0);
+  perm_swap<m>(__int_as_float(dhi(a)), __int_as_float(dhi(b)), l1, h1);
+  lo = djoin(__float_as_int(l0), __float_as_int(l1));
+  hi = djoin(__float_as_int(h0), __float_as_int(h1));
+}
+__device__ __forceinline__ double max_raw(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // The xor 32 (16) reduction stage of two values at once: lanes 0-31 (rows
 // 0, 2) receive a's lower + upper halves (rows), lanes 32-63 (rows 1, 3) b's
-template <int m, bool MAX>
-__device__ __forceinline__ float swap_op(float a, float b) {
-  float lo, hi;
+template <int m, bool MAX, typename T>
+__device__ __forceinline__ T swap_op(T a, T b) {
+  T lo, hi;
   perm_swap<m>(a, b, lo, hi);
   return MAX ? max_raw(lo, hi) : lo + hi;
 }
 __device__ __forceinline__ float readlane_f32(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_f32(double v, int l) {
+  return djoin(__builtin_amdgcn_readlane(dlo(v), l), __builtin_amdgcn_readlane(dhi(v), l));
+}
+// binary64 row stages: each half moved by the same DPP control, then one op
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  return djoin(__builtin_amdgcn_mov_dpp(dlo(x), CTRL, 0xF, 0xF, true),
+               __builtin_amdgcn_mov_dpp(dhi(x), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<kRor8>(v);
+  v += dpp_f64<kRor4>(v);
+  v += dpp_f64<kQuadX2>(v);
+  v += dpp_f64<kQuadX1>(v);
+  return v;
+}
+__device__ __forceinline__ double row_max16(double v) {
+  v = max_raw(v, dpp_f64<kRor8>(v));
+  v = max_raw(v, dpp_f64<kRor4>(v));
+  v = max_raw(v, dpp_f64<kQuadX2>(v));
+  v = max_raw(v, dpp_f64<kQuadX1>(v));
+  return v;
 }
 
 // Reductions of CB per-codeword wave values together (binary32): codeword
@@ -218,23 +264,23 @@ __device__ __forceinline__ float readlane_f32(float v, int l) {
 // permlane16 stage (one codeword per 16-lane row: 0, 2, 1, 3), then one row
 // reduction serves all; the same operand pairs in the same order as
 // wave_sum / wave_max per codeword, so the same bits.  Results are uniform.
-template <bool MAX, int CB>
-__device__ __forceinline__ void wave_reduce_cb(float (&v)[CB]) {
+template <bool MAX, int CB, typename T>
+__device__ __forceinline__ void wave_reduce_cb(T (&v)[CB]) {
   static_assert(CB == 1 || CB == 2 || CB == 4, "codewords per reduction");
   if constexpr (CB == 1) {
-    float p = swap_op<32, MAX>(v[0], v[0]);
+    T p = swap_op<32, MAX>(v[0], v[0]);
     p = swap_op<16, MAX>(p, p);
     v[0] = readlane_f32(MAX ? row_max16(p) : row_sum16(p), 0);
   } else if constexpr (CB == 2) {
-    float p = swap_op<32, MAX>(v[0], v[1]);
+    T p = swap_op<32, MAX>(v[0], v[1]);
     p = swap_op<16, MAX>(p, p);
     p = MAX ? row_max16(p) : row_sum16(p);
     v[0] = readlane_f32(p, 0);
     v[1] = readlane_f32(p, 32);
   } else {
-    const float p01 = swap_op<32, MAX>(v[0], v[1]);
-    const float p23 = swap_op<32, MAX>(v[2], v[3]);
-    float q = swap_op<16, MAX>(p01, p23);
+    const T p01 = swap_op<32, MAX>(v[0], v[1]);
+    const T p23 = swap_op<32, MAX>(v[2], v[3]);
+    T q = swap_op<16, MAX>(p01, p23);
     q = MAX ? row_max16(q) : row_sum16(q);
     v[0] = readlane_f32(q, 0);
     v[2] = readlane_f32(q, 16);
@@ -295,12 +341,12 @@ __device__ __forceinline__ void bfly_bank_f32(float (&x)[E]) {
 // their upper ones in another, an add and a sub form the outputs, a second
 // swap puts them back in place: four VALU ops per two elements instead of six
 // (lower lanes a + b, upper a - b, as before).
-template <int m, int E>
-__device__ __forceinline__ void bfly_swap_f32(float (&x)[E]) {
+template <int m, typename real, int E>
+__device__ __forceinline__ void bfly_swap(real (&x)[E]) {
   static_assert(E % 2 == 0, "pairs");
 #pragma unroll
   for (int i = 0; i < E; i += 2) {
-    float a, b;
+    real a, b;
     perm_swap<m>(x[i], x[i + 1], a, b);
     perm_swap<m>(a + b, a - b, x[i], x[i + 1]);
   }
@@ -313,8 +359,8 @@ __device__ __forceinline__ void lane_butterfly(real (&x)[E], int lane) {
   const real sg = (lane & m) ? (real)-1 : (real)1;
   if constexpr ((m == 4 || m == 8) && sizeof(real) == 4) {
     bfly_bank_f32<m, E>(x);
-  } else if constexpr ((m == 16 || m == 32) && sizeof(real) == 4 && E % 2 == 0) {
-    bfly_swap_f32<m, E>(x);
+  } else if constexpr ((m == 16 || m == 32) && E % 2 == 0) {
+    bfly_swap<m, real, E>(x);
   } else if constexpr ((m == 16 || m == 32) && sizeof(real) == 4) {
     // v_permlane{16,32}_swap of x with itself leaves a = the lower partner
     // and b = the upper one in every lane: lower lanes a + b, upper a - b
@@ -338,7 +384,7 @@ __device__ __forceinline__ void lane_butterfly(real (&x)[E], int lane) {
 // Full-wave xor-butterfly reductions (fixed order: deterministic bits).
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-  if constexpr (sizeof(T) == 4 && (T)0.5 != 0) {  // binary32: fused stages, same pairs
+  if constexpr ((T)0.5 != 0) {  // floating point: fused stages, same pairs
     v = swap_op<32, false>(v, v);
     v = swap_op<16, false>(v, v);
     return row_sum16(v);
@@ -354,8 +400,8 @@ __device__ __forceinline__ T wave_sum(T v) {
 
 template <typename T>
 __device__ __forceinline__ void wave_sum2(T& a, T& b) {
-  if constexpr (sizeof(T) == 4 && (T)0.5 != 0) {  // binary32: both in one register after xor 32
-    float v[2] = {a, b};
+  if constexpr ((T)0.5 != 0) {  // floating point: both in one register after xor 32
+    T v[2] = {a, b};
     wave_reduce_cb<false, 2>(v);
     a = v[0];
     b = v[1];
@@ -371,8 +417,8 @@ __device__ __forceinline__ void wave_sum2(T& a, T& b) {
 
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
-  if constexpr (sizeof(T) == 4 && (T)0.5 != 0) {  // binary32
-    float r[1] = {v};
+  if constexpr ((T)0.5 != 0) {  // floating point
+    T r[1] = {v};
     wave_reduce_cb<true, 1>(r);
     return r[0];
   }
@@ -384,11 +430,6 @@ __device__ __forceinline__ T wave_max(T v) {
   o = xor_lane<2>(v); v = o > v ? o : v;
   o = xor_lane<1>(v); v = o > v ? o : v;
   return v;
-}
-template <bool MAX, int CB>
-__device__ __forceinline__ void wave_reduce_cb(double (&v)[CB]) {
-#pragma unroll
-  for (int c = 0; c < CB; ++c) v[c] = MAX ? wave_max(v[c]) : wave_sum(v[c]);
 }
 
 // In-wave natural-order Walsh-Hadamard transform of one section.
@@ -450,8 +491,8 @@ __device__ __forceinline__ void fwht_wave_sgn(float (&x)[E], float s1, float s2)
         : "v"(s1), "v"(s2));
   bfly_bank_f32<4, E>(x);
   bfly_bank_f32<8, E>(x);
-  bfly_swap_f32<16, E>(x);
-  bfly_swap_f32<32, E>(x);
+  bfly_swap<16, float, E>(x);
+  bfly_swap<32, float, E>(x);
 }
 
 template <typename real> __device__ __forceinline__ real dsqrt(real x);
@@ -2004,41 +2045,41 @@ __global__ void __launch_bounds__(kRowWaves * 64) k_row(RowArgs<real> a) {
   if (lane == 0) a.zzp[(size_t)b * a.NZ + blockIdx.x] = s;
 }
 
-// k_row with V-float accesses (binary32, n % V == 0, many codewords; V = 4:
-// 16 bytes, 256 rows per workgroup; V = 2: 8 bytes, 128 rows): V rows per
-// lane, so each load instruction of the partial stream moves 64 V floats per
-// wave (k_row: 64).  Per row the same sums as k_row in the same order (wave w
+// k_row with V-element accesses (n % V == 0, many codewords; binary32 V = 4:
+// 16 bytes, 256 rows per workgroup, or V = 2: 8 bytes, 128 rows; binary64
+// V = 2: 16 bytes, 128 rows): V rows per lane, so each load instruction of
+// the partial stream moves 64 V elements per wave (k_row: 64).  Per row the same sums as k_row in the same order (wave w
 // adds its partial range in order, the four wave sums are added in wave
 // order); the z^2 partials cover 64 V rows.
-template <int V>
-__global__ void __launch_bounds__(256) k_rowv(RowArgs<float> a) {
-  using fv = float __attribute__((ext_vector_type(V)));
+template <typename real, int V>
+__global__ void __launch_bounds__(256) k_rowv(RowArgs<real> a) {
+  using fv = real __attribute__((ext_vector_type(V)));
   __shared__ fv red[4][64];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = a.n;
   const int r = blockIdx.x * 64 * V + lane * V;  // the lane's first row
   const bool in = r < n;                          // n % V == 0: V rows or none
-  float tau = 1, last = 0;
+  real tau = 1, last = 0;
   if (a.mode == ROW_AMP) {
     tau = ld_vmem(a.tau + (size_t)b * a.T1 + a.t);
-    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : 0.f;
+    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   }
   const size_t o = (size_t)b * n + (in ? r : 0);
   fv yv = {}, zv = {};
-  float bbv[2] = {0.f, 0.f};
+  real bbv[2] = {0, 0};
   if (wv == 0) {
     yv = *reinterpret_cast<const fv*>(a.y + o);
     if (a.mode == ROW_AMP) {
       zv = *reinterpret_cast<const fv*>(a.z + o);
-      const float* bp = a.bbp + (size_t)b * a.Gb;
-      bbv[0] = lane < a.Gb ? bp[lane] : 0.f;
-      bbv[1] = lane + 64 < a.Gb ? bp[lane + 64] : 0.f;
+      const real* bp = a.bbp + (size_t)b * a.Gb;
+      bbv[0] = lane < a.Gb ? bp[lane] : (real)0;
+      bbv[1] = lane + 64 < a.Gb ? bp[lane + 64] : (real)0;
     }
   }
   if (a.mode != ROW_INIT0) {
     const int gq = (a.G + 3) / 4;
     const int g0 = wv * gq, g1 = min(a.G, g0 + gq);
-    const float* p = a.abp + (size_t)b * a.G * n + (in ? r : 0);
+    const real* p = a.abp + (size_t)b * a.G * n + (in ? r : 0);
     fv acc = {};
     constexpr int U = 8;
     for (int gg = g0; gg < g1; gg += U) {
@@ -2053,13 +2094,13 @@ __global__ void __launch_bounds__(256) k_rowv(RowArgs<float> a) {
     red[wv][lane] = acc;
   }
   if (a.mode == ROW_AMP && a.early_stop && tau == last) return;  // uniform over the workgroup
-  const float tau2 = tau * tau;
+  const real tau2 = tau * tau;
   __syncthreads();
   if (wv != 0) return;
-  float ons = 0;
+  real ons = 0;
   if (a.mode == ROW_AMP) {
-    const float bb = a.Gb <= 128 ? wave_sum_pair(bbv[0], bbv[1]) : wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
-    ons = a.Pb[(size_t)b * a.Pbst] - bb / (float)n;
+    const real bb = a.Gb <= 128 ? wave_sum_pair(bbv[0], bbv[1]) : wave_sum_parts(a.bbp + (size_t)b * a.Gb, a.Gb);
+    ons = a.Pb[(size_t)b * a.Pbst] - bb / (real)n;
   }
   fv zn = {};
   if (in) {
@@ -2080,10 +2121,10 @@ __global__ void __launch_bounds__(256) k_rowv(RowArgs<float> a) {
     *reinterpret_cast<fv*>(a.z + o) = zn;
   }
   if (a.mode == ROW_ABOUT) return;
-  float q = 0;
+  real q = 0;
 #pragma unroll
   for (int j = 0; j < V; ++j) q += zn[j] * zn[j];
-  const float s = wave_sum(q);
+  const real s = wave_sum(q);
   if (lane == 0) a.zzp[(size_t)b * a.NZ + blockIdx.x] = s;
 }
 
@@ -2967,12 +3008,15 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
 // their blocks cover the CUs twice, else k_row (64 rows).
 int row_kind_for(const sa_ctx* c, int B) {
   if ((long long)B * c->NZ < 4LL * c->n_cus) return 1;
-  if (c->prec == SA_PREC_F32 && c->n % 4 == 0 && (long long)B * c->NZ4 >= 2LL * c->n_cus) return 2;
-  if (c->prec == SA_PREC_F32 && c->n % 2 == 0 && (long long)B * c->NZ2 >= 2LL * c->n_cus) return 3;
+  const bool f32 = c->prec == SA_PREC_F32;
+  // 16-byte rows: binary32 n % 4 == 0 (256-row blocks) or binary64 n even (128)
+  if (c->n % (f32 ? 4 : 2) == 0 && (long long)B * (f32 ? c->NZ4 : c->NZ2) >= 2LL * c->n_cus) return 2;
+  if (f32 && c->n % 2 == 0 && (long long)B * c->NZ2 >= 2LL * c->n_cus) return 3;  // 8-byte rows
   return 0;
 }
 int nz_for(const sa_ctx* c, int kind) {
-  return kind == 1 ? c->NZ16 : (kind == 2 ? c->NZ4 : (kind == 3 ? c->NZ2 : c->NZ));
+  const bool f32 = c->prec == SA_PREC_F32;
+  return kind == 1 ? c->NZ16 : (kind == 2 ? (f32 ? c->NZ4 : c->NZ2) : (kind == 3 ? c->NZ2 : c->NZ));
 }
 void pick_row(sa_ctx* c, int B) {
   c->row_kind = row_kind_for(c, B);
@@ -2987,12 +3031,12 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb) {
   // workgroups, 4 waves with deeper per-lane load streams
   if (c->row_kind == 1) {
     PROF_REPS(c) k_row2<real><<<dim3(c->NZ16, B), 16 * kRow2Rows, 0, c->stream>>>(a);
-  } else if (c->row_kind >= 2) {
+  } else if (c->row_kind == 2) {
+    constexpr int V = 16 / (int)sizeof(real);  // 16-byte rows
+    PROF_REPS(c) k_rowv<real, V><<<dim3(c->nz_cur, B), 256, 0, c->stream>>>(a);
+  } else if (c->row_kind == 3) {
     if constexpr (sizeof(real) == 4) {
-      if (c->row_kind == 2)
-        PROF_REPS(c) k_rowv<4><<<dim3(c->NZ4, B), 256, 0, c->stream>>>(a);
-      else
-        PROF_REPS(c) k_rowv<2><<<dim3(c->NZ2, B), 256, 0, c->stream>>>(a);
+      PROF_REPS(c) k_rowv<float, 2><<<dim3(c->NZ2, B), 256, 0, c->stream>>>(a);
     } else {
       return SA_ERR_UNSUPPORTED;  // never chosen for binary64 (row_kind_for)
     }

@@ -484,7 +484,7 @@ def test_c2_batch256_golden(sp):
     B = 256
     op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp32")
     plan = op.plan(B)
-    assert plan["section_kernel"] == "k_secb" and plan["row_kernel"] == "k_rowv4", plan
+    assert plan["section_kernel"] == "k_secb" and plan["row_kernel"] == "k_rowv16B", plan
     Pl = float(g["P"]) / L * np.ones(L)
     oAb, oAz, _ = orc.sparc_transforms(L, M, n)
     sigma = float(g["sigma"])

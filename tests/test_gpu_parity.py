@@ -268,6 +268,30 @@ def test_batch_matches_single_and_deterministic(sp, prec, L, M, B):
         assert rel(b6[i], ref) <= TOL[prec]
 
 
+@pytest.mark.parametrize("prec,n,want", [("fp32", 1024, "k_rowv16B"), ("fp32", 1026, "k_rowv8B"),
+                                         ("fp64", 1026, "k_rowv16B"), ("fp32", 1025, "k_row"),
+                                         ("fp64", 1025, "k_row")])
+def test_row_kernel_variants_vs_oracle(sp, prec, n, want):
+    """Every batched row kernel (the Onsager residual of sparc_ldpc.py:220 and
+    the A beta sum of :143-146): k_rowv with 16-byte rows (binary32 n % 4 == 0,
+    binary64 n even), with 8-byte rows (binary32 n even), k_row for odd n; each
+    chosen at B = 128 and checked against the oracle codeword by codeword."""
+    L, M, B, P, T = 128, 256, 128, 2.0, 4
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=prec)
+    assert op.plan(B)["row_kernel"] == want, op.plan(B)
+    Pl = P / L * np.ones(L)
+    Ab, Az, _ = orc.sparc_transforms(L, M, n)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.6, Ab, 900 + i)[1].reshape(-1) for i in range(B)])
+    bb, _ = op.amp_batch(ys, Pl, T, early_stop=False)
+    for i in (0, 1, 63, B - 1):
+        ref = orc._amp_core(ys[i].reshape(-1, 1), Pl, L, M, T, Ab, Az, None, early_stop=False)[0]
+        assert rel(bb[i], ref) <= TOL[prec], i
+        assert argmax_agree(bb[i], ref, L, M)
+    ab = op.Ab_batch(bb)  # the row kernel's A beta output mode
+    for i in (0, B - 1):
+        assert rel(ab[i], Ab(bb[i].reshape(-1, 1))) <= TOL[prec]
+
+
 @pytest.mark.parametrize("prec", ["fp32", "fp64"])
 def test_c2_batched_golden(sp, prec):
     """The golden C2 codeword decoded inside a batch of 6 (batched kernel)."""

@@ -851,9 +851,12 @@ __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
 // issued before the z barrier so their latency overlaps.
 #ifdef SA_STAMPS
 __device__ unsigned long long g_stamps[16];
+#ifndef SA_STAMP_BLOCK
+#define SA_STAMP_BLOCK 0  // the workgroup whose phases are stamped (-DSA_STAMP_BLOCK=gridDim.x-1: the last)
+#endif
 #define STAMP(i)                                                                        \
   do {                                                                                  \
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {                       \
+    if (blockIdx.x == SA_STAMP_BLOCK && blockIdx.y == 0 && threadIdx.x == 0) {          \
       __builtin_amdgcn_sched_barrier(0);                                                \
       unsigned long long _t;                                                            \
       asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");       \
@@ -922,9 +925,17 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     }
   } else {
     // Every load that does not depend on z is issued together with the z
-    // loads (one round trip): z (16-B loads, whole 4 KB chunks), the first
-    // bucket-table chunk, the previous beta, c_l, the first Ab-table rows and
-    // the z^2 partials for tau.
+    // loads (one round trip), in the order they are needed (vmcnt retires
+    // them in order): the z^2 partials and tau_{t-1} for the stop test, z
+    // (16-B loads, whole 4 KB chunks), the first bucket-table chunk, the
+    // previous beta, c_l, the first Ab-table rows.
+    const real* zzb = a.zzp + (size_t)b * a.NZ;
+    ZZParts<real> zz;
+    real last = 0;
+    if (a.mode == SEC_AMP) {
+      zz.issue(zzb, a.NZ, lane);
+      if (a.t > 0) last = ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1);
+    }
     const real* zb = a.z + (size_t)b * n;
     ZStage<real> zst;
     const bool dma = stage_z_dma<real, 256>(zb, zs, n, tid);
@@ -941,8 +952,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
     }
     real tau2 = 1;
     if (a.mode == SEC_AMP) {
-      const real tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, n);
-      const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
+      const real tau = zz.tau(zzb, a.NZ, n);
       const bool stop = a.early_stop && (tau == last);
       if (blockIdx.x == 0 && tid == 0) {
         a.tau[(size_t)b * a.T1 + a.t] = tau;
@@ -1672,6 +1682,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   ZZParts<real, F64 ? 2 : 3> zzc[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) zzc[c].issue(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, lane);
+  // tau_{t-1} of the CB codewords (the exact-tau stop) right behind them: a
+  // load issued after the table loads would make the stop test wait for all
+  // of them (vmcnt retires in order), one more round trip per codeword
+  real lastv[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
   // z rows of the CB codewords (first pass of the staging loop)
   constexpr int KZ = 4;
   real zr[KZ][CB];
@@ -1716,8 +1732,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     const real tau = zzc[c].tau(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
-    const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
-    const bool stop = a.early_stop && (tau == last);
+    const bool stop = a.early_stop && (tau == lastv[c]);
     if (valid[c] && g == 0 && tid == 0) {
       a.tau[(size_t)bc[c] * a.T1 + a.t] = tau;
       if (stop && a.iters[bc[c]] < 0) a.iters[bc[c]] = a.t;

@@ -77,9 +77,6 @@ __device__ __forceinline__ T ld_vmem(const T* p) {
   return p[z0];
 }
 
-// Store of a partial another kernel reads after the boundary (Ab partials):
-// non-temporal, so no dirty L2 line is left for the kernel-end writeback to
-// drain (c2: k_sec4 7.85 -> 7.65 us, +1.5 % codewords/s; c3 neutral).
 // load at a uniform base + 32-bit byte offset (SGPR-base addressing, no
 // 64-bit address arithmetic per load)
 template <typename T>
@@ -87,6 +84,9 @@ __device__ __forceinline__ T ld_off(const T* base, unsigned byte_off) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
+// Store of a partial another kernel reads after the boundary (Ab partials):
+// non-temporal, so no dirty L2 line is left for the kernel-end writeback to
+// drain (c2: k_sec4 7.85 -> 7.65 us, +1.5 % codewords/s; c3 neutral).
 template <typename T>
 __device__ __forceinline__ void st_part(T* p, T v) {
   __builtin_nontemporal_store(v, p);
@@ -632,8 +632,14 @@ __device__ __forceinline__ void load_section(const real* p, real (&x)[E], int la
       const float4 t = *reinterpret_cast<const float4*>(p + e0);
       x[i] = t.x; x[i + 1] = t.y; x[i + 2] = t.z; x[i + 3] = t.w;
     } else {
+      // unconditional loads (clamped index, masked after): a load inside a
+      // branch keeps the compiler from counting the loads in flight, and a
+      // later wait for an earlier load then becomes a wait for all of them
 #pragma unroll
-      for (int q = 0; q < Q; ++q) x[i + q] = e0 + q < M ? p[e0 + q] : (real)0;
+      for (int q = 0; q < Q; ++q) {
+        const real t = p[e0 + q < M ? e0 + q : 0];
+        x[i + q] = e0 + q < M ? t : (real)0;
+      }
     }
   }
 }
@@ -751,8 +757,9 @@ struct ZStage {
     nv = ((reinterpret_cast<uintptr_t>(zb) & 15) == 0) ? n / V : 0;
     const vec_t* zv = reinterpret_cast<const vec_t*>(zb);
     const int last = nv > 0 ? nv - 1 : 0;
-#define SA_ZU_LOAD(u) if (u * NT < nv) { const int j = u * NT + tid; t##u = zv[j < nv ? j : last]; }
-    if (nv > 0) { SA_ZU_EACH(SA_ZU_LOAD) }
+    // unconditional (clamped): straight-line loads the compiler can count
+#define SA_ZU_LOAD(u) { const int j = u * NT + tid; t##u = zv[j < nv ? j : last]; }
+    SA_ZU_EACH(SA_ZU_LOAD)
 #undef SA_ZU_LOAD
   }
   __device__ __forceinline__ void store(real* zs, const real* zb, int n, int tid) const {
@@ -774,6 +781,9 @@ struct ZStage {
 // 7.51 -> 7.26 us, +2 % codewords/s.
 template <typename real, int NT>
 __device__ __forceinline__ bool stage_z_dma(const real* zb, real* zs, int n, int tid) {
+#ifdef SA_NO_DMA
+  return false;
+#endif
   if (reinterpret_cast<uintptr_t>(zb) & 15) return false;
   const int lane = tid & 63, nbytes = n * (int)sizeof(real);
   for (int ch = tid >> 6; ch * 1024 < nbytes; ch += NT / 64) {
@@ -1341,23 +1351,28 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   ushort4 tb[KH][NQ];
   uint32_t f[KR];
 
-  // loads in the order they are needed (vmcnt retires them in order)
-  const real* zzb = a.zzp + (size_t)b * a.NZ;
-  ZZParts<real> zz;
-  zz.issue(zzb, a.NZ, lane);
-  const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
+  // Load order: z's LDS-DMA first, then the z^2 partials and tau_{t-1}, then
+  // the tables, all unconditional (straight-line).  While an LDS-DMA is in
+  // flight the compiler waits for any loaded register with vmcnt(0) (checked
+  // on a minimal kernel), so tau waits for every load whatever the order; the
+  // earliest possible DMA (z is the last thing the gather needs) and no
+  // branches around loads measured c2 1316 -> 1372 cw/s (k_sec4 7.45 ->
+  // 6.68 us); register-staged z with exact waits instead: 1337
   const real* zb = a.z + (size_t)b * n;
   ZStage<real, NT> zst;
   const bool dma = stage_z_dma<real, NT>(zb, zs, n, tid);
   if (!dma) zst.issue(zb, n, tid);
+  const real* zzb = a.zzp + (size_t)b * a.NZ;
+  ZZParts<real> zz;
+  zz.issue(zzb, a.NZ, lane);
+  const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
   load_section<real, EQ>(bl, bprev, lane, Mq);
   const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
-  const int nk = min(KR, (n + NT - 1) / NT);
 #pragma unroll
-  for (int u = 0; u < KR; ++u) {
+  for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
     const int r = u * NT + tid;
-    if (u < nk) f[u] = fw[r < n ? r : 0];
+    f[u] = fw[r < n ? r : 0];
   }
   const real tau = zz.tau(zzb, a.NZ, n);
   const bool stop = a.early_stop && (tau == last);

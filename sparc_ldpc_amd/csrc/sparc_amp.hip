@@ -504,6 +504,9 @@ template <typename real> __device__ __forceinline__ real dexp(real x);
 // instead of the ~10-instruction range-reduced expf
 template <> __device__ __forceinline__ float dexp<float>(float x) { return __expf(x); }
 template <> __device__ __forceinline__ double dexp<double>(double x) { return exp(x); }
+// 1/x to about 1 ulp in one instruction (binary32 v_rcp_f32); binary64 keeps the division
+__device__ __forceinline__ float rcp_fast(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double rcp_fast(double x) { return 1.0 / x; }
 template <typename real> __device__ __forceinline__ real neg_inf();
 template <> __device__ __forceinline__ float neg_inf<float>() { return -INFINITY; }
 template <> __device__ __forceinline__ double neg_inf<double>() { return -INFINITY; }
@@ -1385,6 +1388,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
     return;
   }
   const real tau2 = tau * tau;
+  // the denoiser's scalars now, off its dependency chain (computed while the
+  // z staging and the bucket gather run)
+  const real inv_sn = (real)1 / a.sqrt_n;
+  const real kk = cl / tau2;
   STAMP(1);
   if (!dma) zst.store(zs, zb, n, tid);
   else finish_z_dma(zb, zs, n, tid);
@@ -1416,8 +1423,8 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   STAMP(4);
 
   // denoiser (sparc_ldpc.py:213-219) over the four quarters of the section
-  const real inv_sn = (real)1 / a.sqrt_n;
-  const real kk = cl / tau2;
+  // (inv_sn, kk: computed after tau)
+
   real mx = neg_inf<real>();
 #pragma unroll
   for (int i = 0; i < EQ; ++i) {
@@ -1444,7 +1451,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   __syncthreads();
   S = combine_q<real, QW, false>(red, w0, 1);
   S2 = combine_q<real, QW, false>(red, w0, 2);
-  const real scale = cl / S;
+  const real scale = cl * rcp_fast(S);  // one v_rcp (1 ulp) instead of a division chain on the critical path
 #pragma unroll
   for (int i = 0; i < EQ; ++i) v[i] = have ? v[i] * scale : (real)0;
   if (have) store_section<real, EQ>(blo, v, lane, Mq);

@@ -20,7 +20,8 @@ CASES = [  # L, M, R, B, precision
     (512, 512, 1.0, 8, "fp32"), (512, 512, 1.0, 3, "fp32"), (512, 512, 1.0, 1, "fp32"),
     (768, 512, 5 / 6, 6, "fp32"), (128, 256, 1.0, 16, "fp32"), (64, 128, 1.0, 8, "fp32"),
     (32, 64, 1.0, 8, "fp32"), (16, 16, 1.0, 8, "fp32"), (512, 512, 1.0, 8, "fp64"),
-    (64, 128, 1.0, 8, "fp64"),
+    (64, 128, 1.0, 8, "fp64"), (768, 512, 5 / 6, 1, "fp32"), (768, 512, 5 / 6, 2, "fp64"),
+    (512, 512, 1.0, 1, "fp64"), (256, 256, 1.0, 2, "fp32"),
 ]
 
 

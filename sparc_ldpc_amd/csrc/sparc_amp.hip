@@ -640,8 +640,12 @@ __device__ __forceinline__ void load_section(const real* p, real (&x)[E], int la
       // later wait for an earlier load then becomes a wait for all of them
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        const real t = p[e0 + q < M ? e0 + q : 0];
-        x[i + q] = e0 + q < M ? t : (real)0;
+        if constexpr (sizeof(real) == 4) {
+          const real t = p[e0 + q < M ? e0 + q : 0];
+          x[i + q] = e0 + q < M ? t : (real)0;
+        } else {  // binary64: the conditional form (the select costs the 128-VGPR batched kernel spills)
+          x[i + q] = e0 + q < M ? p[e0 + q] : (real)0;
+        }
       }
     }
   }
@@ -1707,9 +1711,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // tau_{t-1} of the CB codewords (the exact-tau stop) right behind them: a
   // load issued after the table loads would make the stop test wait for all
   // of them (vmcnt retires in order), one more round trip per codeword
+  // (binary64 keeps the late load: at 128 VGPRs the early one costs spills)
   real lastv[CB];
+  if constexpr (!F64) {
 #pragma unroll
-  for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+    for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+  }
   // z rows of the CB codewords (first pass of the staging loop)
   constexpr int KZ = 4;
   real zr[KZ][CB];
@@ -1754,6 +1761,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     const real tau = zzc[c].tau(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
+    if constexpr (F64) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
     const bool stop = a.early_stop && (tau == lastv[c]);
     if (valid[c] && g == 0 && tid == 0) {
       a.tau[(size_t)bc[c] * a.T1 + a.t] = tau;

@@ -1332,7 +1332,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   constexpr int NT = SPW * QW * 64;
   constexpr int KH = EQ >= 8 ? 4 : 16;
   constexpr int NQ = (EQ + 3) / 4;
-  constexpr int KR = (4608 + NT - 1) / NT;  // rows per thread per pass: n <= 4608 in one pass
+  // rows per thread per pass, all Ab-table loads issued with the first loads: n <= 4608 (pairs,
+  // C2) / 8448 (triples, C4 n = 8294) in one pass (a second pass reloads the table mid-phase:
+  // one more memory round trip)
+  constexpr int KR = ((SPW == 3 ? 8448 : 4608) + NT - 1) / NT;
   const int g = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int sidx = wv / QW, q = wv % QW;

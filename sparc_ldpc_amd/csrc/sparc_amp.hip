@@ -1863,7 +1863,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       // <= 1 ulp of u, inside the parity bounds; 4 % faster at c3)
       const real u = fma(v[c][i], inv_sn, bprev[PB ? c : (c & 1)][i]) * k;
       v[c][i] = (E >= 2 || elem_index<E>(lane, i) < M) ? u : neg_inf<real>();
-      m = v[c][i] > m ? v[c][i] : m;
+      m = max_raw(m, v[c][i]);  // one v_max (operands finite or -inf)
     }
     mx[c] = m;
   }

@@ -764,6 +764,10 @@ struct SecArgs {
   int L, M, n, w, nhi, G, NZ, T1, t, mode, early_stop;
   int cst;  // codeword stride of c: 0 (one power allocation) or L (sa_stage_power_batch)
   int RS;  // row splits: RS workgroups share a section group, each gathers n/RS rows of Ab
+  // Ab partial layout of the multi-wave single-codeword kernels: 0 [B][G][n];
+  // 1 row-block major [B][ceil(n/32)][G][32] (k_row2 reads one contiguous
+  // G x 128-B block per workgroup)
+  int pt;
   int B, NC;  // batched kernel: codewords, codeword chunks of CB
   real sqrt_n;
 };
@@ -1411,11 +1415,6 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
   load_section<real, EQ>(bl, bprev, lane, Mq);
   const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
-#pragma unroll
-  for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
-    const int r = u * NT + tid;
-    f[u] = fw[r < n ? r : 0];
-  }
   const real tau = zz.tau(zzb, a.NZ, n);
   const bool stop = a.early_stop && (tau == last);
   if (g == 0 && tid == 0) {
@@ -1456,6 +1455,16 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
     }
   }
   real* xs = xb + sidx * M;
+  // the Ab-table rows (not needed before the row phase) issued only now: they
+  // land under the transforms and the denoiser, where no other load is in
+  // flight, instead of adding their bytes (C2 18 KB, C4 33 KB per workgroup)
+  // to the first memory round trip, which every wave waits for (C4 single
+  // codeword 860 -> 894 cw/s, c2 1378 -> 1394; `k_sec43` 11.0 -> 10.7 us)
+#pragma unroll
+  for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
+    const int r = u * NT + tid;
+    f[u] = fw[r < n ? r : 0];
+  }
   STAMP(3);
   fwht_wave<real, EQ>(v, lane, 64);
   topq_stage<real, EQ, QW>(v, xs, lane, q);
@@ -1515,6 +1524,8 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   }
   // Ab partial of the pair (triple) for every row
   real* abp = a.abp + ((size_t)b * a.G + g) * n;
+  const size_t npad = (size_t)((n + 31) >> 5) << 5;
+  real* abq = a.abp + (size_t)b * a.G * npad + ((size_t)g << 5);  // pt: + (r >> 5) * G * 32 + (r & 31)
   for (int r0 = 0; r0 < n; r0 += NT * KR) {
     if (r0 > 0) {  // n > NT * KR only
 #pragma unroll
@@ -1542,7 +1553,8 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
           t += (e & 0x80000u) ? -v1 : v1;
           t += (e & 0x20000000u) ? -v2 : v2;
         }
-        st_part(&abp[r], t);
+        if (a.pt) st_part(&abq[(size_t)(r >> 5) * ((size_t)a.G << 5) + (r & 31)], t);
+        else st_part(&abp[r], t);
       }
     }
   }
@@ -2043,6 +2055,7 @@ struct RowArgs {
   // [B] per codeword (sa_stage_power_batch, Pbst = 1) or one shared value (Pbst = 0)
   const real* __restrict__ Pb;
   int Pbst;
+  int pt;  // Ab partial layout (SecArgs::pt); k_row2 only
 };
 
 // Residual update with the Onsager term (sparc_ldpc.py:220):
@@ -2242,7 +2255,11 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
     }
   }
   if (a.mode != ROW_INIT0) {
-    const real* p = a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
+    // pt: partial g of row r at [b][r / 32][g][r % 32] (n padded to 32 rows)
+    const size_t gs = a.pt ? (size_t)kRow2Rows : (size_t)n;
+    const real* p = a.pt ? a.abp + (size_t)b * a.G * ((size_t)gridDim.x * kRow2Rows) +
+                               (size_t)blockIdx.x * a.G * kRow2Rows + rl
+                         : a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
     real acc = 0;
     constexpr int U = 16;
     for (int g0 = pg; g0 < a.G; g0 += 16 * U) {
@@ -2250,7 +2267,7 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int g = g0 + 16 * u;
-        t[u] = p[(size_t)(g < a.G ? g : pg) * n];
+        t[u] = p[(size_t)(g < a.G ? g : pg) * gs];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -2648,6 +2665,7 @@ struct sa_ctx {
   bool sec3 = false;   // k_sec43 (three sections x 4 waves per workgroup) chosen over k_sec4
   size_t sec3_lds = 0;
   uint32_t* d_fwd3 = nullptr;
+  bool pt_on = false;  // row-block-major Ab partials between k_sec4 / k_sec43 and k_row2 (SecArgs::pt)
   bool sec4 = false;   // k_sec4 (4 waves per section) fits and is chosen
   size_t sec4_lds = 0;
   int NZ16 = 0;        // k_row2 16-row blocks; nz_cur = z^2 partial count of the current decode
@@ -2841,7 +2859,8 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   if ((rc = dev_alloc(c, &c->d_z, nB * c->n * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_beta, nB * LM * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_out, nB * (LM > (size_t)c->n ? LM : (size_t)c->n) * s))) return rc;
-  if ((rc = dev_alloc(c, &c->d_abp, (size_t)nB * Gmax * c->n * s))) return rc;
+  // rows padded to 32: the row-block-major layout of the pair / triple kernels (SecArgs::pt)
+  if ((rc = dev_alloc(c, &c->d_abp, (size_t)nB * Gmax * ((size_t)c->NZ16 * kRow2Rows) * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_bbp, (size_t)nB * Gmax * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZ16 * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_tau, (size_t)nB * (nT + 1) * s))) return rc;
@@ -2863,7 +2882,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
     const size_t LMs = (size_t)c->L * c->M * s;
     void* bufs[] = {c->d_y, c->d_z, c->d_beta, c->d_out, c->d_abp, c->d_bbp, c->d_zzp, c->d_tau};
     const size_t sz[] = {nB * c->n * s, nB * c->n * s, nB * LMs, nB * (LMs > (size_t)c->n * s ? LMs : (size_t)c->n * s),
-                         (size_t)nB * Gmax * c->n * s, (size_t)nB * Gmax * s,
+                         (size_t)nB * Gmax * ((size_t)c->NZ16 * kRow2Rows) * s, (size_t)nB * Gmax * s,
                          (size_t)nB * c->NZ16 * s, (size_t)nB * (nT + 1) * s};
     for (int i = 0; i < 8; ++i)
       if (mask & (1 << i)) HIP_TRY(hipMemsetAsync(bufs[i], 0xff, sz[i], c->stream));
@@ -2922,6 +2941,7 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   a.L = c->L; a.M = c->M; a.n = c->n; a.w = c->w; a.nhi = c->nhi; a.G = c->G; a.NZ = c->nz_cur;
   a.T1 = c->Tcap + 1; a.t = t; a.mode = mode; a.early_stop = early_stop;
   a.RS = 1;
+  a.pt = 0;
   a.B = 0; a.NC = 0;
   a.cst = c->pb_on ? c->L : 0;
   if (c->pb_on) a.c = (const real*)c->d_cb;
@@ -2942,6 +2962,7 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb
   a.sqrt_n = c->backend != SA_BACKEND_HADAMARD ? (real)1 : (real)std::sqrt((double)c->n);
   a.Pb = c->pb_on ? (const real*)c->d_Pb : (const real*)c->d_P1;
   a.Pbst = c->pb_on ? 1 : 0;
+  a.pt = 0;
   return a;
 }
 
@@ -3020,8 +3041,9 @@ bool use_sec2(const sa_ctx* c, int B) {
 int sec2_parts(const sa_ctx* c) { return c->sec3 ? c->G3 : c->G2; }
 
 template <typename real>
-int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout) {
+int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout, int pt = 0) {
   SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
+  a.pt = pt;
   a.beta = (real*)bin;
   a.beta_out = (real*)bout;
   a.G = sec2_parts(c);
@@ -3104,8 +3126,9 @@ void pick_row(sa_ctx* c, int B) {
 }
 
 template <typename real>
-int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb) {
+int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt = 0) {
   RowArgs<real> a = row_args<real>(c, mode, t, es, G, Gb);
+  a.pt = pt;
   if (c->prof) c->prof->begin(c->stream, K_ROW);
   // small batch: 16-row workgroups cover the chip; many codewords: 64-row
   // workgroups, 4 waves with deeper per-lane load streams
@@ -3296,6 +3319,8 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
   pick_row(c, B);  // row kernel and its z^2 partial count
+  // Ab partials row-block major between the pair / triple kernels and k_row2
+  const int pt = (sec2 && (c->sec3 || c->sec4) && c->row_kind == 1 && c->pt_on) ? 1 : 0;
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
   const int G = i8 ? S8 : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
@@ -3336,12 +3361,12 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
       void* pin = (t & 1) ? c->d_beta2 : c->d_beta;
       void* pout = (t & 1) ? c->d_beta : c->d_beta2;
       if (sec2) {
-        if ((rc = launch_sec2<real>(c, B, t, es, pin, pout))) return rc;
+        if ((rc = launch_sec2<real>(c, B, t, es, pin, pout, pt))) return rc;
       } else if ((rc = launch_sec<real>(c, B, SEC_AMP, t, es, pin, pout))) {
         return rc;
       }
     }
-    if ((rc = launch_row<real>(c, B, ROW_AMP, t, es, G, Gb))) return rc;
+    if ((rc = launch_row<real>(c, B, ROW_AMP, t, es, G, Gb, pt))) return rc;
   }
   k_iters_final<<<(B + 255) / 256, 256, 0, c->stream>>>(c->d_iters, B, T);
   HIP_TRY(hipGetLastError());
@@ -3661,6 +3686,8 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       c->sec4 = true;
       c->sec4_lds = need4;
     }
+    const char* ept = getenv("SPARC_AMP_PT");
+    c->pt_on = ept && ept[0] == '1';
   }
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for

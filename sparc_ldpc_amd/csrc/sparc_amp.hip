@@ -3686,8 +3686,12 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       c->sec4 = true;
       c->sec4_lds = need4;
     }
+    // row-block-major Ab partials for k_row2 (SPARC_AMP_PT=0: the [G][n] layout):
+    // each k_row2 workgroup reads one contiguous G x 128-B block instead of G
+    // lines n rows apart.  C4 single codeword 880 -> 950 cw/s (k_row2 4.1 ->
+    // 3.4 us, two interleaved A/B rounds); c2 within noise
     const char* ept = getenv("SPARC_AMP_PT");
-    c->pt_on = ept && ept[0] == '1';
+    c->pt_on = !(ept && ept[0] == '0');
   }
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for

@@ -415,6 +415,30 @@ def test_triple_section_kernel(sp, prec, L, M, n, monkeypatch):
         assert argmax_agree(b3[0], orc.amp(y, 0, Pl, L, M, 30, oAb, oAz), L, M)
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+@pytest.mark.parametrize("L,M,n,sec3", [(512, 512, 4608, "0"), (300, 512, 6007, "1"), (258, 256, 2581, "0")])
+def test_partial_layouts_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
+    """The row-block-major Ab partials between k_sec4 / k_sec43 and k_row2
+    (the default) and the [G][n] layout (SPARC_AMP_PT=0) hold the same sums in
+    the same order: decodes bit-identical, incl. n not a multiple of the
+    32-row block; and against the oracle."""
+    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
+    Pl = 2.0 / L * np.ones(L)
+    y = orc.rep_inputs(L, M, n, Pl, 0.9, oAb, 77)[1].reshape(-1)
+    monkeypatch.setenv("SPARC_AMP_SEC3", sec3)
+    ops = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SPARC_AMP_PT", flag)
+        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
+    assert ops["1"].plan(1)["section_kernel"] == ("k_sec43" if sec3 == "1" else "k_sec4")
+    for t in (1, 4):
+        b1, i1 = ops["1"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+        b0, i0 = ops["0"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+        assert np.array_equal(b1, b0) and np.array_equal(i1, i0), t
+        ref, _ = orc.amp_test(y, 0, Pl, L, M, t, oAb, oAz)
+        assert rel(b1[0], ref) <= TOL[prec], t
+
+
 def test_c4_single_uses_triples(sp):
     """L=768 M=512 R=5/6 (n=8294) single codeword: the triple kernel is the
     default where pairs overfill the chip (ceil(L/2) > CUs >= ceil(L/3))."""

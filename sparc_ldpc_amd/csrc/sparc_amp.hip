@@ -1409,7 +1409,14 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   const bool dma = stage_z_dma<real, NT>(zb, zs, n, tid);
   if (!dma) zst.issue(zb, n, tid);
   const real* zzb = a.zzp + (size_t)b * a.NZ;
-  ZZParts<real> zz;
+  // z^2 partials held in registers: k_row2 writes ceil(n / 32) (C4 n = 8294:
+  // 260, past the 256 of K = 4, whose fallback re-reads them: one more memory
+  // round trip before tau), k_row2<16> ceil(n / 16) (C2: 288)
+#ifdef SA_R16_TRIPLE
+  ZZParts<real, SPW == 3 ? 9 : 5> zz;
+#else
+  ZZParts<real, 5> zz;
+#endif
   zz.issue(zzb, a.NZ, lane);
   const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
@@ -1524,8 +1531,9 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   }
   // Ab partial of the pair (triple) for every row
   real* abp = a.abp + ((size_t)b * a.G + g) * n;
-  const size_t npad = (size_t)((n + 31) >> 5) << 5;
-  real* abq = a.abp + (size_t)b * a.G * npad + ((size_t)g << 5);  // pt: + (r >> 5) * G * 32 + (r & 31)
+  const int psh = a.pt == 16 ? 4 : 5;  // pt: rows per block 16 / 32
+  const size_t npad = (size_t)((n + (1 << psh) - 1) >> psh) << psh;
+  real* abq = a.abp + (size_t)b * a.G * npad + ((size_t)g << psh);  // pt: + (r >> psh) * G * R + (r & (R - 1))
   for (int r0 = 0; r0 < n; r0 += NT * KR) {
     if (r0 > 0) {  // n > NT * KR only
 #pragma unroll
@@ -1553,7 +1561,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
           t += (e & 0x80000u) ? -v1 : v1;
           t += (e & 0x20000000u) ? -v2 : v2;
         }
-        if (a.pt) st_part(&abq[(size_t)(r >> 5) * ((size_t)a.G << 5) + (r & 31)], t);
+        if (a.pt) st_part(&abq[(size_t)(r >> psh) * ((size_t)a.G << psh) + (r & ((1 << psh) - 1))], t);
         else st_part(&abp[r], t);
       }
     }
@@ -2228,12 +2236,15 @@ __global__ void __launch_bounds__(256) k_rowv(RowArgs<real> a) {
 // (all loads of a thread in flight together); the 16 group sums are added in
 // group order; wave 0 finishes the rows (Onsager residual, z^2 partial).
 constexpr int kRow2Rows = 32;  // one 128-B line of a partial per row block
-template <typename real>
+// R = 16 (row-block-major partials only, where the line holds two partials of
+// the same block): twice the workgroups, NG = 32 partial groups of G / 32
+template <typename real, int R = kRow2Rows>
 __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
-  __shared__ real red[16][kRow2Rows + 1];
+  constexpr int NG = 512 / R;  // partial groups
+  __shared__ real red[NG][R + 1];
   const int b = blockIdx.y, tid = threadIdx.x;
-  const int rl = tid & (kRow2Rows - 1), pg = tid >> 5;
-  const int r = blockIdx.x * kRow2Rows + rl;
+  const int rl = tid & (R - 1), pg = tid / R;
+  const int r = blockIdx.x * R + rl;
   const int n = a.n;
   // tau_t and tau_{t-1} are loaded with everything else; the early-stop
   // test waits for them only after the Ab-partial loads are in flight
@@ -2255,23 +2266,23 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
     }
   }
   if (a.mode != ROW_INIT0) {
-    // pt: partial g of row r at [b][r / 32][g][r % 32] (n padded to 32 rows)
-    const size_t gs = a.pt ? (size_t)kRow2Rows : (size_t)n;
-    const real* p = a.pt ? a.abp + (size_t)b * a.G * ((size_t)gridDim.x * kRow2Rows) +
-                               (size_t)blockIdx.x * a.G * kRow2Rows + rl
+    // pt: partial g of row r at [b][r / R][g][r % R] (n padded to R rows)
+    const size_t gs = a.pt ? (size_t)R : (size_t)n;
+    const real* p = a.pt ? a.abp + (size_t)b * a.G * ((size_t)gridDim.x * R) +
+                               (size_t)blockIdx.x * a.G * R + rl
                          : a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
     real acc = 0;
-    constexpr int U = 16;
-    for (int g0 = pg; g0 < a.G; g0 += 16 * U) {
+    constexpr int U = 256 / NG;  // G = 256 (C2, C4): every load of a thread in one pass
+    for (int g0 = pg; g0 < a.G; g0 += NG * U) {
       real t[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int g = g0 + 16 * u;
+        const int g = g0 + NG * u;
         t[u] = p[(size_t)(g < a.G ? g : pg) * gs];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (g0 + 16 * u < a.G) acc += t[u];
+        if (g0 + NG * u < a.G) acc += t[u];
     }
     red[pg][rl] = acc;
   }
@@ -2293,13 +2304,13 @@ __global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
     ons = a.Pb[(size_t)b * a.Pbst] - bb / (real)n;
   }
   real zn = 0;
-  if (tid < kRow2Rows && r < n) {
+  if (tid < R && r < n) {
     if (a.mode == ROW_INIT0) {
       zn = yv;
     } else {
       real acc = 0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc += red[q][rl];
+      for (int q = 0; q < NG; ++q) acc += red[q][rl];
       const real ab = acc / a.sqrt_n;
       if (a.mode == ROW_ABOUT) {
         a.out[o] = ab;
@@ -2668,7 +2679,9 @@ struct sa_ctx {
   bool pt_on = false;  // row-block-major Ab partials between k_sec4 / k_sec43 and k_row2 (SecArgs::pt)
   bool sec4 = false;   // k_sec4 (4 waves per section) fits and is chosen
   size_t sec4_lds = 0;
-  int NZ16 = 0;        // k_row2 16-row blocks; nz_cur = z^2 partial count of the current decode
+  int NZ16 = 0;        // k_row2 32-row blocks; nz_cur = z^2 partial count of the current decode
+  int NZh = 0;         // k_row2 16-row blocks (row16)
+  bool row16 = false;  // k_row2<16> after k_sec4 (row-block-major partials, NZh <= 320)
   int NZ4 = 0, NZ2 = 0;  // k_rowv<4> 256-row / k_rowv<2> 128-row blocks
   int row_kind = 0;    // row kernel of the current decode: 0 k_row, 1 k_row2, 2 k_rowv<4>, 3 k_rowv<2>
   int nz_cur = 0;
@@ -2862,7 +2875,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   // rows padded to 32: the row-block-major layout of the pair / triple kernels (SecArgs::pt)
   if ((rc = dev_alloc(c, &c->d_abp, (size_t)nB * Gmax * ((size_t)c->NZ16 * kRow2Rows) * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_bbp, (size_t)nB * Gmax * s))) return rc;
-  if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZ16 * s))) return rc;
+  if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZh * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_tau, (size_t)nB * (nT + 1) * s))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_iters, (size_t)nB * sizeof(int)))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_stop, (size_t)nB * sizeof(int)))) return rc;
@@ -2883,7 +2896,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
     void* bufs[] = {c->d_y, c->d_z, c->d_beta, c->d_out, c->d_abp, c->d_bbp, c->d_zzp, c->d_tau};
     const size_t sz[] = {nB * c->n * s, nB * c->n * s, nB * LMs, nB * (LMs > (size_t)c->n * s ? LMs : (size_t)c->n * s),
                          (size_t)nB * Gmax * ((size_t)c->NZ16 * kRow2Rows) * s, (size_t)nB * Gmax * s,
-                         (size_t)nB * c->NZ16 * s, (size_t)nB * (nT + 1) * s};
+                         (size_t)nB * c->NZh * s, (size_t)nB * (nT + 1) * s};
     for (int i = 0; i < 8; ++i)
       if (mask & (1 << i)) HIP_TRY(hipMemsetAsync(bufs[i], 0xff, sz[i], c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -3109,7 +3122,7 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
 // 4 CUs, else in binary32 k_rowv<4> (n % 4 == 0) or k_rowv<2> (n even) when
 // their blocks cover the CUs twice, else k_row (64 rows).
 int row_kind_for(const sa_ctx* c, int B) {
-  if ((long long)B * c->NZ < 4LL * c->n_cus) return 1;
+  if ((long long)B * c->NZ < 4LL * c->n_cus) return (c->row16 && B == 1) ? 4 : 1;
   const bool f32 = c->prec == SA_PREC_F32;
   // 16-byte rows: binary32 n % 4 == 0 (256-row blocks) or binary64 n even (128)
   if (c->n % (f32 ? 4 : 2) == 0 && (long long)B * (f32 ? c->NZ4 : c->NZ2) >= 2LL * c->n_cus) return 2;
@@ -3118,6 +3131,7 @@ int row_kind_for(const sa_ctx* c, int B) {
 }
 int nz_for(const sa_ctx* c, int kind) {
   const bool f32 = c->prec == SA_PREC_F32;
+  if (kind == 4) return c->NZh;
   return kind == 1 ? c->NZ16 : (kind == 2 ? (f32 ? c->NZ4 : c->NZ2) : (kind == 3 ? c->NZ2 : c->NZ));
 }
 void pick_row(sa_ctx* c, int B) {
@@ -3133,7 +3147,9 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt 
   // small batch: 16-row workgroups cover the chip; many codewords: 64-row
   // workgroups, 4 waves with deeper per-lane load streams
   if (c->row_kind == 1) {
-    PROF_REPS(c) k_row2<real><<<dim3(c->NZ16, B), 16 * kRow2Rows, 0, c->stream>>>(a);
+    PROF_REPS(c) k_row2<real><<<dim3(c->NZ16, B), 512, 0, c->stream>>>(a);
+  } else if (c->row_kind == 4) {
+    PROF_REPS(c) k_row2<real, 16><<<dim3(c->NZh, B), 512, 0, c->stream>>>(a);
   } else if (c->row_kind == 2) {
     constexpr int V = 16 / (int)sizeof(real);  // 16-byte rows
     PROF_REPS(c) k_rowv<real, V><<<dim3(c->nz_cur, B), 256, 0, c->stream>>>(a);
@@ -3320,7 +3336,8 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const bool sec2 = use_sec2(c, B);
   pick_row(c, B);  // row kernel and its z^2 partial count
   // Ab partials row-block major between the pair / triple kernels and k_row2
-  const int pt = (sec2 && (c->sec3 || c->sec4) && c->row_kind == 1 && c->pt_on) ? 1 : 0;
+  const int pt = (sec2 && (c->sec3 || c->sec4) && (c->row_kind == 1 || c->row_kind == 4) && c->pt_on)
+                     ? (c->row_kind == 4 ? 16 : kRow2Rows) : 0;
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
   const int G = i8 ? S8 : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
@@ -3660,6 +3677,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   if (ordering) c->ordering.assign(ordering, ordering + (size_t)L * n);
   c->NZ = (n + kRowsPerBlk - 1) / kRowsPerBlk;
   c->NZ16 = (n + kRow2Rows - 1) / kRow2Rows;
+  c->NZh = (n + 15) / 16;
   c->NZ4 = (n + 255) / 256;
   c->NZ2 = (n + 127) / 128;
   c->nz_cur = c->NZ;
@@ -3692,6 +3710,16 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     // 3.4 us, two interleaved A/B rounds); c2 within noise
     const char* ept = getenv("SPARC_AMP_PT");
     c->pt_on = !(ept && ept[0] == '0');
+    // 16-row k_row2 blocks for one codeword where the z^2 partials still fit
+    // the section kernels' registers (ceil(n / 16) <= 320; C2: 288 workgroups
+    // instead of 144, every CU pulls partials): c2 1362-1374 -> 1396 cw/s
+    // (two interleaved A/B rounds).  SPARC_AMP_R16=0: 32-row blocks
+    const char* er = getenv("SPARC_AMP_R16");
+#ifdef SA_R16_TRIPLE
+    c->row16 = !(er && er[0] == '0') && c->pt_on && c->sec4 && c->NZh <= 576;
+#else
+    c->row16 = !(er && er[0] == '0') && c->pt_on && c->sec4 && c->NZh <= 320;
+#endif
   }
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for

@@ -421,22 +421,33 @@ def test_partial_layouts_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
     """The row-block-major Ab partials between k_sec4 / k_sec43 and k_row2
     (the default) and the [G][n] layout (SPARC_AMP_PT=0) hold the same sums in
     the same order: decodes bit-identical, incl. n not a multiple of the
-    32-row block; and against the oracle."""
+    32-row block; and against the oracle.  The default 16-row k_row2 blocks
+    (ceil(n / 16) <= 320; 32 partial groups instead of 16) against the oracle."""
     oAb, oAz, oord = orc.sparc_transforms(L, M, n)
     Pl = 2.0 / L * np.ones(L)
     y = orc.rep_inputs(L, M, n, Pl, 0.9, oAb, 77)[1].reshape(-1)
     monkeypatch.setenv("SPARC_AMP_SEC3", sec3)
+    monkeypatch.setenv("SPARC_AMP_R16", "0")  # 32-row blocks in both layouts: the same sums
     ops = {}
     for flag in ("1", "0"):
         monkeypatch.setenv("SPARC_AMP_PT", flag)
         ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
+    monkeypatch.delenv("SPARC_AMP_PT")
+    monkeypatch.delenv("SPARC_AMP_R16")
+    ops["16"] = sp.SparcOperator(L, M, n, oord, precision=prec)  # the default: 16-row blocks where they fit
     assert ops["1"].plan(1)["section_kernel"] == ("k_sec43" if sec3 == "1" else "k_sec4")
+    assert ops["1"].plan(1)["row_kernel"] == "k_row2"
+    assert ops["16"].plan(1)["row_kernel"] == ("k_row2_16" if (n + 15) // 16 <= 320 else "k_row2")
     for t in (1, 4):
         b1, i1 = ops["1"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
         b0, i0 = ops["0"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
         assert np.array_equal(b1, b0) and np.array_equal(i1, i0), t
         ref, _ = orc.amp_test(y, 0, Pl, L, M, t, oAb, oAz)
         assert rel(b1[0], ref) <= TOL[prec], t
+        b16, _ = ops["16"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+        b16b, _ = ops["16"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+        assert np.array_equal(b16, b16b), t  # bitwise reproducible
+        assert rel(b16[0], ref) <= TOL[prec], t
 
 
 def test_c4_single_uses_triples(sp):

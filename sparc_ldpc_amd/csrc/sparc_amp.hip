@@ -1412,11 +1412,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   // z^2 partials held in registers: k_row2 writes ceil(n / 32) (C4 n = 8294:
   // 260, past the 256 of K = 4, whose fallback re-reads them: one more memory
   // round trip before tau), k_row2<16> ceil(n / 16) (C2: 288)
-#ifdef SA_R16_TRIPLE
-  ZZParts<real, SPW == 3 ? 9 : 5> zz;
-#else
   ZZParts<real, 5> zz;
-#endif
   zz.issue(zzb, a.NZ, lane);
   const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
   load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
@@ -3715,11 +3711,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     // instead of 144, every CU pulls partials): c2 1362-1374 -> 1396 cw/s
     // (two interleaved A/B rounds).  SPARC_AMP_R16=0: 32-row blocks
     const char* er = getenv("SPARC_AMP_R16");
-#ifdef SA_R16_TRIPLE
-    c->row16 = !(er && er[0] == '0') && c->pt_on && c->sec4 && c->NZh <= 576;
-#else
     c->row16 = !(er && er[0] == '0') && c->pt_on && c->sec4 && c->NZh <= 320;
-#endif
   }
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for

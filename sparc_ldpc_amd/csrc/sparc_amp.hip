@@ -1366,7 +1366,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = SPW * QW * 64;
-  constexpr int KH = EQ >= 8 ? 4 : 16;
+  // bucket h-steps whose table loads are in flight together: triples take 8
+  // (C4, 32 h-steps: half the first round trip's table bytes, the rest lands
+  // during the gather; 961 -> 996 cw/s), pairs 16 (c2: all 16 up front; 8 neutral)
+  constexpr int KH = EQ >= 8 ? 4 : (SPW == 3 ? 8 : 16);
   constexpr int NQ = (EQ + 3) / 4;
   // rows per thread per pass, all Ab-table loads issued with the first loads: n <= 4608 (pairs,
   // C2) / 8448 (triples, C4 n = 8294) in one pass (a second pass reloads the table mid-phase:

@@ -2237,9 +2237,9 @@ __global__ void __launch_bounds__(256) k_rowv(RowArgs<real> a) {
 constexpr int kRow2Rows = 32;  // one 128-B line of a partial per row block
 // R = 16 (row-block-major partials only, where the line holds two partials of
 // the same block): twice the workgroups, NG = 32 partial groups of G / 32
-template <typename real, int R = kRow2Rows>
-__global__ void __launch_bounds__(512) k_row2(RowArgs<real> a) {
-  constexpr int NG = 512 / R;  // partial groups
+template <typename real, int R = kRow2Rows, int NT = 512>
+__global__ void __launch_bounds__(NT) k_row2(RowArgs<real> a) {
+  constexpr int NG = NT / R;  // partial groups
   __shared__ real red[NG][R + 1];
   const int b = blockIdx.y, tid = threadIdx.x;
   const int rl = tid & (R - 1), pg = tid / R;

@@ -90,18 +90,20 @@ def i8_gemm_ops(L, M, n, B, planes):
     return 2 * planes * B * n * L * M
 
 
-def _cpu_worker(args):
-    """One host process: build the oracle operator (untimed), then time Tsample
-    AMP iterations of one codeword; returns the wall-clock span."""
+def _cpu_worker(args, barrier, q):
+    """One host process: build the oracle operator (untimed), wait at the
+    barrier for every other process, then time Tsample AMP iterations of one
+    codeword; puts its (start, end) wall-clock span."""
     L, M, n, P, sigma, Tsample, seed = args
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import amp_oracle as orc
     Ab, Az, _ = orc.sparc_transforms(L, M, n)
     Pl = P / L * np.ones(L)
     _, y = orc.rep_inputs(L, M, n, Pl, sigma, Ab, seed)
+    barrier.wait()  # every process starts its timed loop together: no spawn / import stagger in the span
     t0 = time.time()
     orc._amp_core(y, Pl, L, M, Tsample, Ab, Az, None, early_stop=False)  # exactly Tsample iterations
-    return t0, time.time()
+    q.put((t0, time.time()))
 
 
 def host_cpus():
@@ -133,9 +135,10 @@ def host_cpus():
 def cpu_baseline(w, procs=None, Tsample=None):
     """The oracle (the reference's algorithm in fp64 NumPy, vectorised FWHT) on
     the host: `procs` independent single-threaded processes (default: every
-    usable core), each timing Tsample AMP iterations of its own codeword; the
-    rate is all iterations over the wall-clock span from the first start to
-    the last finish, scaled to T iterations per codeword."""
+    usable core), each timing Tsample AMP iterations of its own codeword after
+    a barrier (set-up untimed); the rate is all iterations over the wall-clock
+    span from the common start to the last finish, scaled to T iterations per
+    codeword."""
     import multiprocessing as mp
     L, M, P, sigma, T = w["L"], w["M"], w["P"], w["sigma"], w["T"]
     n = n_of(w)
@@ -143,8 +146,14 @@ def cpu_baseline(w, procs=None, Tsample=None):
     procs = procs or use
     Tsample = Tsample or T  # a whole decode per process: no extrapolation
     ctx = mp.get_context("spawn")
-    with ctx.Pool(procs) as pool:
-        spans = pool.map(_cpu_worker, [(L, M, n, P, sigma, Tsample, 1000 + i) for i in range(procs)])
+    barrier, q = ctx.Barrier(procs), ctx.Queue()
+    ps = [ctx.Process(target=_cpu_worker, args=((L, M, n, P, sigma, Tsample, 1000 + i), barrier, q))
+          for i in range(procs)]
+    for p in ps:
+        p.start()
+    spans = [q.get(timeout=600) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
     wall = max(e for _, e in spans) - min(s for s, _ in spans)
     per_core = float(np.mean([e - s for s, e in spans])) / Tsample
     return {
@@ -212,6 +221,29 @@ def valu_bound(tag, kernel, kernel_ms, cus, clock_ghz=2.4):
             "source": src, "clock_ghz_assumed": clock_ghz}
 
 
+PROFILE_TAGS = {  # (workload, codewords, backend) -> scripts/profile_r*.sh tag (binary32)
+    ("c2", 1, "hadamard"): "c2", ("c4", 1, "hadamard"): "c4b1", ("c3", 256, "hadamard"): "c3",
+    ("c4", 256, "hadamard"): "c4", ("c3", 256, "dense"): "c3dense", ("c4", 1, "dense"): "dense_l768",
+}
+
+
+def load_graph_median(tag, kernel):
+    """In-graph launch duration of `kernel` (ns): the median over the
+    graph-replayed decodes of the newest committed
+    profiles/<round>_<tag>_graph_trace.txt (rocprofv3 kernel trace of the same
+    bench command, scripts/graph_trace.py), with that file's name; or None."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{tag}_graph_trace.txt")))
+    if not files:
+        return None
+    for line in open(files[-1]):
+        m = re.match(r"(\S+)\s+n=\s*(\d+)\s+duration median\s+(\d+) ns", line)
+        if m and m.group(1) == kernel:
+            return float(m.group(3)), int(m.group(2)), os.path.relpath(files[-1], ROOT)
+    return None
+
+
 def load_pmc(workload, kernel):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -237,10 +269,16 @@ def main():
     ap.add_argument("--no-fp64", action="store_true", help="skip the binary64 leg of an fp32 run")
     args = ap.parse_args()
 
-    import sparc_ldpc_amd as sp
     from sparc_ldpc_amd import dist
 
     rank, world, local = dist.env_rank()
+    if args.gpus != world:
+        # a launch without torchrun (or with another rank count) would print an
+        # honest n_gpus = WORLD_SIZE line for a job nobody asked for: refuse it
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 as "
+              f"python -m torch.distributed.run --nproc-per-node N bench.py --gpus N", file=sys.stderr)
+        sys.exit(2)
+    import sparc_ldpc_amd as sp
     # one rank per GPU over RCCL (librccl through ctypes, no PyTorch); the
     # rehearsal mode SPARC_DIST_BACKEND=socket puts several ranks on one GPU
     # (device LOCAL_RANK % device count) with the CPU all-reduce instead
@@ -306,27 +344,47 @@ def main():
     mfma = plan["section_kernel"] == "dense_mfma"
     achieved = per[dom] / (dom_ms * 1e-3) / (1e12 if mfma else 1e9)
     peak = I8_PEAK_TOPS if mfma else HBM_PEAK_GBS
-    pmc = load_pmc(f"{args.workload}_{args.backend}_{args.precision}_B{B}",
-                   {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom))
     kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom)
+    # the kernel's name in the rocprofv3 traces (k_gemm_i8 is one template, two products)
+    trace_name = {"k_dense_az": "k_gemm_i8_Az", "k_dense_ab": "k_gemm_i8_Ab"}[dom] if mfma else kname
+    pmc = load_pmc(f"{args.workload}_{args.backend}_{args.precision}_B{B}", trace_name)
     if mfma:
         kname = "k_gemm_i8 (" + {"k_dense_az": f"A^T z, {NP_Z} digit planes",
                                  "k_dense_ab": f"A beta, {NP_B} digit planes"}[dom] + ")"
+    scale = 1e12 if mfma else 1e9
+    # headline: the launch duration INSIDE the replayed decode graph (the
+    # rocprofv3 graph-trace median of this same bench command, committed under
+    # profiles/), where the kernel follows the row kernel's writes on other
+    # XCDs; beside it the live HIP-event figure of REP back-to-back launches
+    # (inputs still in the caches from the previous launch: a few % faster)
+    tag = PROFILE_TAGS.get((args.workload, B, args.backend)) if args.precision == "fp32" else None
+    gm = load_graph_median(tag, trace_name) if tag else None
+    ev = {"achieved": round(achieved, 1), "frac": round(achieved / peak, 4), "avg_launch_ms": round(dom_ms, 5),
+          "timing": f"HIP events on the library stream around {PROFILE_REP} back-to-back launches per kernel, "
+                    f"measured live in this run"}
+    if gm is not None:
+        g_ms = gm[0] * 1e-6
+        ach_g = per[dom] / (g_ms * 1e-3) / scale
+        head = {"achieved": round(ach_g, 1), "frac": round(ach_g / peak, 4), "avg_launch_ms": round(g_ms, 5),
+                "timing": f"in-graph launch duration: median of {gm[1]} graph-replayed launches, rocprofv3 "
+                          f"kernel trace of this bench command ({gm[2]})"}
+    else:
+        head = ev
     roofline = {
-        "bound": "mfma" if mfma else "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": peak,
-        "unit": "TFLOP/s" if mfma else "GB/s", "frac": round(achieved / peak, 4),
+        "bound": "mfma" if mfma else "hbm", "kernel": kname, "achieved": head["achieved"], "peak": peak,
+        "unit": "TFLOP/s" if mfma else "GB/s", "frac": head["frac"],
         "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
         ("algorithmic_int8_ops_per_launch" if mfma else "algorithmic_bytes_per_launch"): per[dom],
         **({"ops": "int8 multiply-adds x 2 (TOP/s)"} if mfma else {}),
-        "avg_launch_ms": round(dom_ms, 5),
+        "avg_launch_ms": head["avg_launch_ms"], "timing": head["timing"],
+        **({"events": ev} if gm is not None else {}),
         "kernel_ms": {k: round(v[0], 5) for k, v in kinds_rep.items() if v[1]},
         "kernel_ms_event_bracketed": {k: round(v[0], 5) for k, v in kinds.items() if v[1]},
-        "timing": f"HIP events on the library stream around {PROFILE_REP} back-to-back launches per kernel",
         "eager_decode_ms": round(total_ms, 3),
     }
 
     if kname == "k_secb" and args.precision == "fp32":
-        vb = valu_bound(args.workload, kname, dom_ms, plan["cus"])
+        vb = valu_bound(args.workload, kname, head["avg_launch_ms"], plan["cus"])
         if vb is not None:
             roofline["secondary_bound"] = dict(bound="valu", **vb)
     result = {

@@ -122,6 +122,9 @@ double sa_run_event_ms(sa_ctx* ctx);
  * quantisation of z / beta0; out[12] = total ms of the sequence.  Leaves the
  * decode's results in place like sa_run. */
 int sa_profile(sa_ctx* ctx, int B, int T, int flags, double* out);
+/* Number of kernel kinds K of sa_profile / sa_profile_rep: `out` holds 2 K + 1
+ * doubles (K = 6 since SA_VERSION 0.2: size buffers from this, not a constant). */
+int sa_profile_kinds(void);
 /* The same with every bracketed launch issued `rep` (1..1024) times back to
  * back between its events: mean = elapsed / rep, i.e. the launch's duration
  * plus the same-stream kernel boundary, without the event packets' dispatch

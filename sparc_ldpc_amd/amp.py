@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .operators import AbOp, AzOp, SparcOperator, host_loop
+from .operators import AbOp, AzOp, SparcOperator, _cached_operator, host_loop
 
 __all__ = ["amp", "amp_test", "amp_batch", "operator_of"]
 
@@ -53,7 +53,11 @@ def _beta0(β, L, M):
 
 
 def _run(y, Pl, L, M, T, Ab, Az, β, early_stop):
-    if not (isinstance(Ab, AbOp) and isinstance(Az, AzOp) and Ab.op is Az.op):
+    if isinstance(Ab, AbOp) and isinstance(Az, AzOp) and Ab.op is not Az.op:
+        # two of this package's operators that do not belong together: a
+        # caller's mistake, not a foreign operator for the host loop
+        raise ValueError("Ab and Az belong to different operators")
+    if not (isinstance(Ab, AbOp) and isinstance(Az, AzOp)):
         # the caller's own operator (sparc_ldpc.py:189 takes any callables)
         if not (callable(Ab) and callable(Az)):
             raise TypeError(f"Ab and Az must be callable; got {type(Ab).__name__}/{type(Az).__name__}")
@@ -80,9 +84,40 @@ def amp(y, σ_n, Pl, L, M, T, Ab, Az, β=None, *, early_stop=True):
     return b
 
 
-def amp_test(y, σ_n, Pl, L, M, T, Ab, Az, β=None, *, early_stop=True):
+def _sibling(Ab, Az, precision):
+    """The same design (ordering, backend, device) as a cached operator of
+    another device precision; None when Ab/Az are not this package's
+    matrix-free operators or already run in `precision`."""
+    if not (isinstance(Ab, AbOp) and isinstance(Az, AzOp) and Ab.op is Az.op):
+        return None
+    op = Ab.op
+    if op.precision == precision or op.backend != "hadamard":
+        return None
+    sib = _cached_operator(op.L, op.M, op.n, op.ordering, op.backend, precision, op.device)
+    return AbOp(sib), AzOp(sib)
+
+
+def amp_test(y, σ_n, Pl, L, M, T, Ab, Az, β=None, *, early_stop=True, precision="fp64"):
     """amp_test.py:14-50 -> (β̂, t): t is the loop index at which the exact
-    τ stop fired, or T-1 when the loop ran out (Python's loop variable)."""
+    τ stop fired, or T-1 when the loop ran out (Python's loop variable).
+
+    The stop index is part of this function's contract, and it depends on
+    the arithmetic: τ repeats exactly once the iterates reach a fixed point
+    to the last ulp (sparc_ldpc.py:204), which binary32 iterates reach
+    earlier than the reference's binary64 ones (C4 codeword 0: t = 38 in
+    binary32 against the reference's 63).  So by default the decode runs in
+    binary64 (``precision="fp64"``: a binary32 operator of this package is
+    swapped for its cached binary64 twin, same design), where t lies within
+    3 iterations of the reference's (tests/test_gpu_parity.py::
+    test_stop_index_vs_reference).  ``precision="operator"`` keeps the
+    operator's own precision (binary32: the stop index of binary32 iterates,
+    bounded in the same test; β̂ within the fp32 contract either way)."""
+    if precision not in ("fp64", "fp32", "operator"):
+        raise ValueError("precision must be 'fp64', 'fp32' or 'operator'")
+    if precision != "operator":
+        sib = _sibling(Ab, Az, precision)
+        if sib is not None:
+            Ab, Az = sib
     b, it = _run(y, Pl, L, M, T, Ab, Az, β, early_stop)
     return b, (it if it < T else T - 1)
 

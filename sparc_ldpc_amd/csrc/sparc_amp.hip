@@ -39,7 +39,8 @@
 
 #include "sparc_amp.h"
 
-#define SA_VERSION "sparc_amp 0.1 gfx950"
+// 0.3: sa_profile / sa_profile_rep write 2 * sa_profile_kinds() + 1 doubles (13 since 0.2)
+#define SA_VERSION "sparc_amp 0.3 gfx950"
 
 namespace {
 
@@ -4302,6 +4303,8 @@ int sa_amp(sa_ctx* c, int B, const double* y, const double* Pl, int T, const dou
 }
 
 int sa_profile(sa_ctx* c, int B, int T, int flags, double* out) { return sa_profile_rep(c, B, T, flags, 1, out); }
+
+int sa_profile_kinds(void) { return K_NKINDS; }
 
 int sa_profile_rep(sa_ctx* c, int B, int T, int flags, int rep, double* out) {
   if (int rc0 = check_op(c, "sa_profile")) return rc0;

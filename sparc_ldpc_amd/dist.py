@@ -200,13 +200,42 @@ _NCCL_SUM, _NCCL_MAX = 0, 2          # ncclRedOp_t (rccl.h)
 _H2D, _D2H = 1, 2                    # hipMemcpyKind
 
 
-def _load_rocm(name):
-    for cand in (name, os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", name)):
+def _load_rocm(stem):
+    """Load a ROCm library by its unversioned stem (``libamdhip64``,
+    ``librccl``): the development symlink ``<stem>.so`` first, then any
+    versioned ``<stem>.so.N`` on the loader path or under ``$ROCM_PATH/lib``
+    (highest major first), so no ROCm major version is hard-coded."""
+    import glob
+    libdir = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
+    cands = [stem + ".so", os.path.join(libdir, stem + ".so")]
+
+    def major(p):
+        tail = p.rsplit(".so.", 1)[-1].split(".")[0]
+        return int(tail) if tail.isdigit() else -1
+    cands += sorted(glob.glob(os.path.join(libdir, stem + ".so.*")), key=major, reverse=True)
+    for cand in cands:
         try:
             return ct.CDLL(cand)
         except OSError:
             continue
-    raise DistError(f"cannot load {name}")
+    raise DistError(f"cannot load {stem}.so (tried {len(cands)} paths)")
+
+
+_UID_BYTES = ct.sizeof(_UniqueId)
+
+
+def uid_bytes(uid: _UniqueId) -> bytes:
+    """All 128 bytes of an ncclUniqueId.  (``bytes(uid.internal)`` would stop
+    at the first NUL: a c_char array field reads as a C string.)"""
+    return ct.string_at(ct.addressof(uid), _UID_BYTES)
+
+
+def uid_from_bytes(raw: bytes) -> _UniqueId:
+    if len(raw) != _UID_BYTES:
+        raise DistError(f"ncclUniqueId: got {len(raw)} bytes, expected {_UID_BYTES}")
+    uid = _UniqueId()
+    ct.memmove(ct.addressof(uid), raw, _UID_BYTES)
+    return uid
 
 
 class RcclComm:
@@ -216,25 +245,29 @@ class RcclComm:
 
     def __init__(self, rdv: Rendezvous, device: int):
         self.rdv = rdv
-        self.hip = hip = _load_rocm("libamdhip64.so.7")
-        self.rccl = rccl = _load_rocm("librccl.so.1")
+        self.hip = hip = _load_rocm("libamdhip64")
+        self.rccl = rccl = _load_rocm("librccl")
         rccl.ncclGetErrorString.restype = ct.c_char_p
+        rccl.ncclGetErrorString.argtypes = [ct.c_int]
+        rccl.ncclGetUniqueId.argtypes = [ct.POINTER(_UniqueId)]
         rccl.ncclCommInitRank.argtypes = [ct.POINTER(ct.c_void_p), ct.c_int, _UniqueId, ct.c_int]
         rccl.ncclAllReduce.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_size_t, ct.c_int, ct.c_int,
                                        ct.c_void_p, ct.c_void_p]
         rccl.ncclCommDestroy.argtypes = [ct.c_void_p]
+        hip.hipSetDevice.argtypes = [ct.c_int]
+        hip.hipMalloc.argtypes = [ct.POINTER(ct.c_void_p), ct.c_size_t]
+        hip.hipStreamCreate.argtypes = [ct.POINTER(ct.c_void_p)]
         hip.hipMemcpyAsync.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_size_t, ct.c_int, ct.c_void_p]
         hip.hipStreamSynchronize.argtypes = [ct.c_void_p]
         hip.hipFree.argtypes = [ct.c_void_p]
         hip.hipStreamDestroy.argtypes = [ct.c_void_p]
         self._hip_ok(hip.hipSetDevice(int(device)), "hipSetDevice")
-        uid = _UniqueId()
         if rdv.rank == 0:
+            uid = _UniqueId()
             self._nccl_ok(rccl.ncclGetUniqueId(ct.byref(uid)), "ncclGetUniqueId")
-            rdv.bcast(bytes(uid.internal))
+            rdv.bcast(uid_bytes(uid))
         else:
-            raw = rdv.bcast(None)
-            ct.memmove(ct.addressof(uid), raw, 128)
+            uid = uid_from_bytes(rdv.bcast(None))
         self.comm = ct.c_void_p()
         self._nccl_ok(rccl.ncclCommInitRank(ct.byref(self.comm), rdv.world, uid, rdv.rank), "ncclCommInitRank")
         self.stream = ct.c_void_p()

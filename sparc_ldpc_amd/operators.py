@@ -207,6 +207,9 @@ class SparcOperator:
         (mean = elapsed / rep; the staged results are then not a decode)."""
         flags = (0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP) | (_lib.SA_FLAG_BETA0 if beta0 else 0)
         nk = len(self.KERNEL_KINDS)
+        if int(self._lib.sa_profile_kinds()) != nk:
+            raise _lib.SparcAmpError(_lib.SA_ERR_UNSUPPORTED, f"libsparc_amp profiles {self._lib.sa_profile_kinds()} kernel kinds, "
+                                f"this module knows {nk}: rebuild the library")
         out = np.zeros(2 * nk + 1)
         check(self._lib.sa_profile_rep(self._ctx, int(B), int(T), flags, int(rep), dptr(out)))
         kinds = {k: (float(out[2 * i]), int(out[2 * i + 1])) for i, k in enumerate(self.KERNEL_KINDS)}

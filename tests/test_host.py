@@ -213,3 +213,17 @@ def test_allreduce_refuses_without_communicator(monkeypatch):
         dist.allreduce_sum(np.array([1], dtype=np.int64))
     monkeypatch.setenv("WORLD_SIZE", "1")
     assert dist.allreduce_sum(np.array([5], dtype=np.int64)).tolist() == [5]
+
+
+def test_amp_refuses_operators_of_two_contexts():
+    """Ab of one operator with Az of another is a caller's mistake: ValueError,
+    not the foreign-callable host loop (object stand-ins; no device needed)."""
+    from sparc_ldpc_amd.operators import AbOp, AzOp
+    import sparc_ldpc_amd as sp
+
+    class _Op:  # attribute holder in place of two SparcOperators
+        L, M, n = 4, 4, 8
+    with pytest.raises(ValueError, match="different operators"):
+        sp.amp(np.zeros(8), 1.0, np.ones(4), 4, 4, 3, AbOp(_Op()), AzOp(_Op()))
+    with pytest.raises(ValueError, match="different operators"):
+        sp.amp_test(np.zeros(8), 1.0, np.ones(4), 4, 4, 3, AbOp(_Op()), AzOp(_Op()))

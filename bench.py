@@ -329,10 +329,13 @@ def main():
     if args.backend == "hadamard":
         G = plan["partials"]  # Ab partials per codeword of the section kernel this batch runs
         wv = op.w
+        sk = plan["section_kernel"]
         per = {
-            "k_sec": sec_bytes(L, M, n, wv, B, G, s, plan["section_kernel"]),
+            "k_sec": sec_bytes(L, M, n, wv, B, G, s, sk.rstrip("f")),
             "k_row": row_bytes(n, B, G, s),
         }
+        if sk.endswith("f"):  # the fused kernel also does the row step (k_row: the last one only)
+            per["k_sec"] += per["k_row"]
     elif plan["section_kernel"] == "dense_mfma":
         per = {"k_dense_az": i8_gemm_ops(L, M, n, B, NP_Z), "k_dense_ab": i8_gemm_ops(L, M, n, B, NP_B)}
     else:

@@ -554,11 +554,13 @@ __device__ __forceinline__ real wave_sum_pair(real a, real b) {
 template <typename real, int K = 4>
 struct ZZParts {
   real v[K];
+  template <bool SC1 = false>
   __device__ __forceinline__ void issue(const real* p, int cnt, int lane) {
 #pragma unroll
     for (int q = 0; q < K; ++q) {
       const int i = lane + 64 * q;
-      v[q] = p[i < cnt ? i : 0];
+      v[q] = SC1 ? __hip_atomic_load(p + (i < cnt ? i : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : p[i < cnt ? i : 0];
     }
   }
   __device__ __forceinline__ real tau(const real* p, int cnt, int n) const {
@@ -773,6 +775,26 @@ struct SecArgs {
   real sqrt_n;
 };
 
+template <typename real>
+struct RowArgs {
+  const real* __restrict__ y;    // [B][n]
+  real* __restrict__ z;          // [B][n] the residual (k_row2: the new one is written here)
+  const real* __restrict__ z_in; // [B][n] k_row2: the previous residual (= z unless the fused path double-buffers it)
+  const real* __restrict__ abp;  // [B][G][n]
+  const real* __restrict__ bbp;  // [B][G]
+  real* __restrict__ zzp;        // [B][NZ]
+  const real* __restrict__ tau;  // [B][T1]
+  real* __restrict__ out;        // [B][n] (ROW_ABOUT)
+  int n, G, Gb, NZ, T1, t, mode, early_stop;  // G Ab partials, Gb beta^2 partials
+  real sqrt_n;
+  // total power P = sum(Pl) read from device memory (never a captured
+  // argument: a graph replayed after set_power must see the new P):
+  // [B] per codeword (sa_stage_power_batch, Pbst = 1) or one shared value (Pbst = 0)
+  const real* __restrict__ Pb;
+  int Pbst;
+  int pt;  // Ab partial layout (SecArgs::pt); k_row2 only
+};
+
 // One workgroup = 4 wavefronts = 4 consecutive sections of one codeword
 // (blockIdx.y).  Per wave: v = bucket gather of z (LDS), FWHT, denoise,
 // FWHT of the new beta (for Ab), staged to LDS.  Then the workgroup gathers
@@ -823,7 +845,8 @@ struct ZStage {
 // issued at once; the barrier that follows waits for it (vmcnt).  Returns
 // false (nothing issued) when z is not 16-B aligned: ZStage then.  c2: k_sec4
 // 7.51 -> 7.26 us, +2 % codewords/s.
-template <typename real, int NT>
+constexpr int kAuxSc1 = 16;  // cache-policy operand of global_load_lds: sc1 (checked in the ISA)
+template <typename real, int NT, int AUX = 0>
 __device__ __forceinline__ bool stage_z_dma(const real* zb, real* zs, int n, int tid) {
 #ifdef SA_NO_DMA
   return false;
@@ -837,17 +860,18 @@ __device__ __forceinline__ bool stage_z_dma(const real* zb, real* zs, int n, int
     // finish_z_dma's store); the tail goes through finish_z_dma
     if (off + 16 <= nbytes)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)((const char*)zb + off),
-                                       (__attribute__((address_space(3))) void*)((char*)zs + ch * 1024), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)((char*)zs + ch * 1024), 16, 0, AUX);
   }
   return true;
 }
 
 // After stage_z_dma: the < 16-B tail of z by ordinary loads, and the zero
 // slot zs[n] (gathered for empty buckets).
-template <typename real>
+template <typename real, bool SC1 = false>
 __device__ __forceinline__ void finish_z_dma(const real* zb, real* zs, int n, int tid) {
   const int n0 = n * (int)sizeof(real) / 16 * 16 / (int)sizeof(real);
-  if (tid < n - n0) zs[n0 + tid] = zb[n0 + tid];
+  if (tid < n - n0)
+    zs[n0 + tid] = SC1 ? __hip_atomic_load(zb + n0 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : zb[n0 + tid];
   if (tid == 0) zs[n] = 0;
 }
 
@@ -1361,8 +1385,151 @@ __device__ __forceinline__ real combine_q(const real* red, int w0, int f) {
   return x[0];
 }
 
-template <typename real, int EQ, int QW, int SPW = 2>
-__device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
+// ---- fused row step: k_row2 of iteration t-1 at the head of the section
+// kernel of iteration t (one codeword; the section workgroups all resident)
+//
+// Two kernels per iteration pay two dependent kernel boundaries.  The fused
+// kernel K_t does the row step of t-1 first (each workgroup one or two row
+// blocks: the Ab partials of K_{t-1}, the Onsager residual, the z^2 partial),
+// publishes its rows of z_t write-through (sc1 stores, every storing wave's
+// vmcnt(0), a workgroup barrier, one agent-scope add to an arrival counter),
+// waits for every workgroup's arrival, and only then stages z_t: the bucket
+// and Ab-table loads of iteration t, which do not depend on z, are in flight
+// during the row step.  z is double-buffered (K_t reads z_{t-1} from one
+// buffer and writes z_t to the other), so no XCD's L2 can hold a line of the
+// buffer the section phase reads from before the hand-off; after it, z_t and
+// the z^2 partials are read with sc1 loads (MI355X_MICROARCH.md, hand-off
+// forms).  The sums are k_row2<R>'s, in k_row2's order: bit for bit the
+// two-kernel path (tests/test_gpu_fused.py).
+// Measured: SLOWER than two launches, c2 1161-1168 against
+// 1367-1396 codewords/s: the hand-off (write-through stores drained, 256
+// arrivals, the poll) takes ~3.3 us where a kernel boundary takes ~1.7, and
+// the row step's loads share the first round trip with the tables.  Kept
+// opt-in (SPARC_AMP_FUSE=1) as the measured alternative; never the default.
+template <typename real>
+struct FuseArgs {
+  RowArgs<real> r;   // row step t-1 in k_row2's meaning: r.t = t-1, r.z_in = z_{t-1}, r.z = z_t (out)
+  unsigned* bar;     // arrival counters: 8, 32 words (128 B) apart, summed by the poll
+  int* err;          // set to 1 when the arrival poll gives up (never expected: a hang guard)
+  unsigned target;   // counter sum once every workgroup of this launch has arrived
+  int NB;            // row blocks of R rows (workgroup g: blocks g and g + gridDim.x)
+};
+
+constexpr int kBarSpinLimit = 1 << 20;  // ~0.1 s of polling, then err and go on
+
+// k_row2<R, 512>'s loads, sums and finish for the (up to) two row blocks of
+// this workgroup: threads 0..511, thread (rl, pg) sums partials pg + NG u of
+// row rl in order, the NG group sums are added in group order by wave 0
+// (first block) / wave 1 (second block).
+template <typename real, int R>
+struct FusedRows {
+  static constexpr int NG = 512 / R, U = 256 / NG;  // G <= 256 partials (host-checked)
+  real t[2][U];
+  real yv, zv, bbv[4], tau, last;
+  int blk1;  // second block or -1
+  __device__ __forceinline__ void issue(const FuseArgs<real>& f, int tid) {
+    const RowArgs<real>& a = f.r;
+    const int rl = tid & (R - 1), pg = (tid / R) % NG;
+    blk1 = blockIdx.x + gridDim.x < f.NB ? blockIdx.x + gridDim.x : -1;
+    tau = ld_vmem(a.tau + a.t);
+    last = a.t > 0 ? ld_vmem(a.tau + a.t - 1) : (real)0;
+    const int wv = tid >> 6, lane = tid & 63;
+    yv = zv = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bbv[q] = 0;
+    if (wv < 2) {  // wave w finishes block w
+      const int blk = (wv == 1 && blk1 >= 0) ? blk1 : blockIdx.x;
+      const int r = blk * R + (lane & (R - 1));
+      const int o = r < a.n ? r : 0;
+      yv = a.y[o];
+      zv = a.z_in[o];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bbv[q] = lane + 64 * q < a.Gb ? a.bbp[lane + 64 * q] : (real)0;
+    }
+    if (tid < 512) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int blk = (k == 1 && blk1 >= 0) ? blk1 : blockIdx.x;
+        const real* p = a.abp + (size_t)blk * a.G * R + rl;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int g = pg + NG * u;
+          t[k][u] = p[(size_t)(g < a.G ? g : pg) * R];
+        }
+      }
+    }
+  }
+  // returns false when the row step is stopped (tau_{t-1} == tau_{t-2}: nothing
+  // changes, no hand-off is needed and the section phase stops as well)
+  __device__ __forceinline__ bool finish(const FuseArgs<real>& f, int tid, real* red) {
+    const RowArgs<real>& a = f.r;
+    if (a.early_stop && tau == last) return false;  // uniform over the grid
+    const real tau2 = tau * tau;
+    const int rl = tid & (R - 1), pg = tid / R;
+    if (tid < 512) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        real acc = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (pg + NG * u < a.G) acc += t[k][u];
+        red[(k * NG + pg) * (R + 1) + rl] = acc;
+      }
+    }
+    __syncthreads();
+    const int wv = tid >> 6, lane = tid & 63;
+    if (wv == 0 || (wv == 1 && blk1 >= 0)) {
+      const int blk = wv == 1 ? blk1 : blockIdx.x;
+      real sacc = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sacc += bbv[q];
+      const real bb = wave_sum(sacc);
+      const real ons = a.Pb[0] - bb / (real)a.n;
+      const int r = blk * R + (lane & (R - 1));
+      real zn = 0;
+      if (lane < R && r < a.n) {
+        real acc = 0;
+#pragma unroll
+        for (int q = 0; q < NG; ++q) acc += red[(wv * NG + q) * (R + 1) + rl];
+        const real ab = acc / a.sqrt_n;
+        zn = yv - ab;
+        zn += (zv / tau2) * ons;
+        __hip_atomic_store(a.z + r, zn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
+      }
+      const real sz = wave_sum(zn * zn);
+      if (lane == 0) __hip_atomic_store(a.zzp + blk, sz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its stores are done
+    }
+    __syncthreads();
+    return true;
+  }
+};
+
+// Arrival of this workgroup and the wait for all of them (one lane polls the
+// eight counters with sc1 loads, s_sleep between polls, bounded).
+template <typename real>
+__device__ __forceinline__ void grid_arrive_wait(const FuseArgs<real>& f, int tid) {
+  if (tid == 0) {
+    __hip_atomic_fetch_add(f.bar + (blockIdx.x & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int spin = 0;; ++spin) {
+      unsigned s = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += __hip_atomic_load(f.bar + i * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s >= f.target) break;
+      if (spin >= kBarSpinLimit) {
+        __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+// FR > 0: the fused kernel (row step of t-1 on FR-row blocks first, see
+// FuseArgs); FR = 0: the section kernel alone.
+template <typename real, int EQ, int QW, int SPW = 2, int FR = 0>
+__device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs<real>* fu = nullptr) {
   static_assert(SPW == 2 || SPW == 3, "sections per workgroup");
   STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1410,18 +1577,43 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   // 6.68 us); register-staged z with exact waits instead: 1337
   const real* zb = a.z + (size_t)b * n;
   ZStage<real, NT> zst;
-  const bool dma = stage_z_dma<real, NT>(zb, zs, n, tid);
-  if (!dma) zst.issue(zb, n, tid);
   const real* zzb = a.zzp + (size_t)b * a.NZ;
   // z^2 partials held in registers: k_row2 writes ceil(n / 32) (C4 n = 8294:
   // 260, past the 256 of K = 4, whose fallback re-reads them: one more memory
   // round trip before tau), k_row2<16> ceil(n / 16) (C2: 288)
   ZZParts<real, 5> zz;
-  zz.issue(zzb, a.NZ, lane);
-  const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
-  load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
-  load_section<real, EQ>(bl, bprev, lane, Mq);
-  const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
+  bool dma;
+  real last, cl;
+  if constexpr (FR > 0) {
+    // row step t-1 first; the tables of iteration t (independent of z) and
+    // the previous beta are issued right behind its loads and land under it
+    FusedRows<real, FR> fr;
+    fr.issue(*fu, tid);
+    load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);
+    load_section<real, EQ>(bl, bprev, lane, Mq);
+    cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {  // the Ab-table rows too (unconditional, clamped)
+      const int r = u * NT + tid;
+      f[u] = fw[r < n ? r : 0];
+    }
+    const bool ran = fr.finish(*fu, tid, reinterpret_cast<real*>(smem));
+    STAMP(11);
+    if (ran) grid_arrive_wait(*fu, tid);
+    STAMP(12);
+    // z_t and the z^2 partials: published in this launch, read with sc1 loads
+    dma = stage_z_dma<real, NT, kAuxSc1>(zb, zs, n, tid);  // host-checked: z is 16-B aligned
+    zz.template issue<true>(zzb, a.NZ, lane);
+    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
+  } else {
+    dma = stage_z_dma<real, NT>(zb, zs, n, tid);
+    if (!dma) zst.issue(zb, n, tid);
+    zz.issue(zzb, a.NZ, lane);
+    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
+    load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
+    load_section<real, EQ>(bl, bprev, lane, Mq);
+    cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
+  }
   const real tau = zz.tau(zzb, a.NZ, n);
   const bool stop = a.early_stop && (tau == last);
   if (g == 0 && tid == 0) {
@@ -1439,7 +1631,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   const real kk = cl / tau2;
   STAMP(1);
   if (!dma) zst.store(zs, zb, n, tid);
-  else finish_z_dma(zb, zs, n, tid);
+  else finish_z_dma<real, (FR > 0)>(zb, zs, n, tid);
   __syncthreads();
   STAMP(2);
 #ifdef SA_STAMPS
@@ -1467,10 +1659,12 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   // flight, instead of adding their bytes (C2 18 KB, C4 33 KB per workgroup)
   // to the first memory round trip, which every wave waits for (C4 single
   // codeword 860 -> 894 cw/s, c2 1378 -> 1394; `k_sec43` 11.0 -> 10.7 us)
+  if constexpr (FR == 0) {
 #pragma unroll
-  for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
-    const int r = u * NT + tid;
-    f[u] = fw[r < n ? r : 0];
+    for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
+      const int r = u * NT + tid;
+      f[u] = fw[r < n ? r : 0];
+    }
   }
   STAMP(3);
   fwht_wave<real, EQ>(v, lane, 64);
@@ -1579,6 +1773,15 @@ __global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) { secq_body<real,
 // puts one workgroup on every CU where pairs leave half the CUs with two.
 template <typename real, int E4>
 __global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real, E4, 4, 3>(a); }
+// The fused kernels (row step of t-1, hand-off, section step of t)
+template <typename real, int E4, int FR>
+__global__ void __launch_bounds__(512) k_sec4f(SecArgs<real> a, FuseArgs<real> f) {
+  secq_body<real, E4, 4, 2, FR>(a, &f);
+}
+template <typename real, int E4, int FR>
+__global__ void __launch_bounds__(768) k_sec43f(SecArgs<real> a, FuseArgs<real> f) {
+  secq_body<real, E4, 4, 3, FR>(a, &f);
+}
 // ---------------------------------------------------------------------------
 // Batched section kernel (B codewords share the operator)
 // ---------------------------------------------------------------------------
@@ -2047,24 +2250,6 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
 #endif
 }
 
-template <typename real>
-struct RowArgs {
-  const real* __restrict__ y;    // [B][n]
-  real* __restrict__ z;          // [B][n]
-  const real* __restrict__ abp;  // [B][G][n]
-  const real* __restrict__ bbp;  // [B][G]
-  real* __restrict__ zzp;        // [B][NZ]
-  const real* __restrict__ tau;  // [B][T1]
-  real* __restrict__ out;        // [B][n] (ROW_ABOUT)
-  int n, G, Gb, NZ, T1, t, mode, early_stop;  // G Ab partials, Gb beta^2 partials
-  real sqrt_n;
-  // total power P = sum(Pl) read from device memory (never a captured
-  // argument: a graph replayed after set_power must see the new P):
-  // [B] per codeword (sa_stage_power_batch, Pbst = 1) or one shared value (Pbst = 0)
-  const real* __restrict__ Pb;
-  int Pbst;
-  int pt;  // Ab partial layout (SecArgs::pt); k_row2 only
-};
 
 // Residual update with the Onsager term (sparc_ldpc.py:220):
 //   z = y - Ab(beta) + (z / tau^2) * (P - sum(beta^2) / n)
@@ -2259,7 +2444,7 @@ __global__ void __launch_bounds__(NT) k_row2(RowArgs<real> a) {
   if (tid < 64) {
     yv = a.y[o];
     if (a.mode == ROW_AMP) {
-      zv = a.z[o];
+      zv = a.z_in[o];
       const real* bp = a.bbp + (size_t)b * a.Gb;
 #pragma unroll
       for (int q = 0; q < 4; ++q) bbv[q] = tid + 64 * q < a.Gb ? bp[tid + 64 * q] : (real)0;
@@ -2364,6 +2549,14 @@ __global__ void k_convert(const src_t* s, dst_t* d, size_t N) {
 __global__ void k_fill32(uint32_t* p, uint32_t v, size_t nw) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x)
     p[i] = v;
+}
+
+// Fused path: the final residual of a codeword lies in the buffer of parity
+// iters[b] (z double-buffered); bring it home to z (one codeword).
+template <typename real>
+__global__ void k_z_final(real* z, const real* z2, const int* it, int n) {
+  if (!(it[0] & 1)) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) z[i] = z2[i];
 }
 
 template <typename real>
@@ -2682,6 +2875,11 @@ struct sa_ctx {
   int NZ16 = 0;        // k_row2 32-row blocks; nz_cur = z^2 partial count of the current decode
   int NZh = 0;         // k_row2 16-row blocks (row16)
   bool row16 = false;  // k_row2<16> after k_sec4 (row-block-major partials, NZh <= 320)
+  bool fuse = false;   // one codeword: the row step of t-1 fused into the section kernel of t (k_sec4f / k_sec43f)
+  void* d_z2 = nullptr;         // the fused path's second residual buffer (z double-buffered)
+  unsigned* d_bar = nullptr;    // the fused path's arrival counters (8 x 128 B)
+  int* d_err = nullptr;         // set by a fused launch whose arrival poll gave up
+  unsigned bar_seq = 0;         // fused launches since the counters were last cleared (host side)
   int NZ4 = 0, NZ2 = 0;  // k_rowv<4> 256-row / k_rowv<2> 128-row blocks
   int row_kind = 0;    // row kernel of the current decode: 0 k_row, 1 k_row2, 2 k_rowv<4>, 3 k_rowv<2>
   int nz_cur = 0;
@@ -2757,6 +2955,9 @@ void free_workspace(sa_ctx* c) {
     *p = nullptr;
   }
   dev_free(c->d_iters); c->d_iters = nullptr;
+  dev_free(c->d_z2); c->d_z2 = nullptr;
+  dev_free(c->d_bar); c->d_bar = nullptr;
+  dev_free(c->d_err); c->d_err = nullptr;
   dev_free(c->d_stop); c->d_stop = nullptr;
   dev_free(c->d_idx); c->d_idx = nullptr;
   dev_free(c->d_beta2); c->d_beta2 = nullptr;
@@ -2882,6 +3083,10 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   if ((rc = dev_alloc(c, (void**)&c->d_idx, (size_t)nB * c->L * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, &c->d_cb, (size_t)nB * c->L * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_Pb, (size_t)nB * s))) return rc;
+  if ((rc = dev_alloc(c, &c->d_z2, (size_t)c->n * s))) return rc;  // one codeword
+  if ((rc = dev_alloc(c, (void**)&c->d_bar, 8 * 128))) return rc;
+  if ((rc = dev_alloc(c, (void**)&c->d_err, sizeof(int)))) return rc;
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
   if (c->backend == SA_BACKEND_DENSE)
     if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->RS * c->lda * sizeof(float)))) return rc;
   if (c->backend == SA_BACKEND_HOST)  // the caller's A^T z, one partial per codeword
@@ -2965,7 +3170,7 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
 template <typename real>
 RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb) {
   RowArgs<real> a;
-  a.y = (const real*)c->d_y; a.z = (real*)c->d_z; a.abp = (const real*)c->d_abp;
+  a.y = (const real*)c->d_y; a.z = (real*)c->d_z; a.z_in = a.z; a.abp = (const real*)c->d_abp;
   a.bbp = (const real*)c->d_bbp; a.zzp = (real*)c->d_zzp; a.tau = (const real*)c->d_tau;
   a.out = (real*)c->d_out;
   a.n = c->n; a.G = G; a.NZ = c->nz_cur;
@@ -3099,6 +3304,81 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout, int pt =
   return SA_OK;
 }
 
+int row_kind_for(const sa_ctx* c, int B);
+// Ab partial layout between the pair / triple kernels and k_row2 (SecArgs::pt):
+// rows per row-major block, 0 for the [G][n] layout
+int pt_for(const sa_ctx* c, int B, bool sec2) {
+  const int rk = row_kind_for(c, B);
+  return (sec2 && (c->sec3 || c->sec4) && (rk == 1 || rk == 4) && c->pt_on) ? (rk == 4 ? 16 : kRow2Rows) : 0;
+}
+
+// The fused path (row step of t-1 + hand-off + section step of t in one
+// launch) for one codeword on the pair / triple kernels with row-block-major
+// partials: every workgroup must be resident at once (one per CU at most),
+// k_row2's single-pass sums (G, Gb <= 256), the z^2 partials in the section
+// kernel's registers (<= 320) and the two row blocks' sums in the z region of LDS.
+int fused_rows(const sa_ctx* c) { return c->row16 ? 16 : kRow2Rows; }
+bool use_fused(const sa_ctx* c, int B, int pt) {
+  if (!c->fuse || B != 1 || pt == 0 || !use_sec2(c, B) || !(c->sec4 || c->sec3)) return false;
+  if (c->M != 256 && c->M != 512) return false;  // instantiated section sizes
+  const int G = sec2_parts(c), R = fused_rows(c);
+  const int NB = R == 16 ? c->NZh : c->NZ16;
+  const size_t zbytes = ((size_t)(c->n + 1) * rsz(c) + 15) / 16 * 16;
+  return pt == R && G <= 256 && G <= c->n_cus && NB <= 2 * G && NB <= 320 &&
+         2 * (512 / R) * (R + 1) * rsz(c) <= zbytes;
+}
+
+template <typename real, int FR>
+void launch_fused_r(sa_ctx* c, const SecArgs<real>& a, FuseArgs<real> f) {
+  dim3 grid(a.G, 1);
+  PROF_REPS(c) {
+    f.target = (unsigned)a.G * ++c->bar_seq;
+    bool done = false;
+    if constexpr (FR == kRow2Rows) {
+      if (c->sec3) {
+        if (c->M == 256) k_sec43f<real, 1, FR><<<grid, 768, c->sec3_lds, c->stream>>>(a, f);
+        else k_sec43f<real, 2, FR><<<grid, 768, c->sec3_lds, c->stream>>>(a, f);
+        done = true;
+      }
+    }
+    if (!done) {
+      if (c->M == 256) k_sec4f<real, 1, FR><<<grid, 512, c->sec4_lds, c->stream>>>(a, f);
+      else k_sec4f<real, 2, FR><<<grid, 512, c->sec4_lds, c->stream>>>(a, f);
+    }
+  }
+}
+
+// K_t (t >= 1): row step t-1 reads z_{t-1} from zin and publishes z_t in zout,
+// the section step t reads zout.
+template <typename real>
+int launch_fused(sa_ctx* c, int t, int es, void* bin, void* bout, void* zin, void* zout, int pt, int G, int Gb) {
+  SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
+  a.pt = pt;
+  a.beta = (real*)bin;
+  a.beta_out = (real*)bout;
+  a.G = sec2_parts(c);
+  a.z = (const real*)zout;
+  FuseArgs<real> f;
+  f.r = row_args<real>(c, ROW_AMP, t - 1, es, G, Gb);
+  f.r.pt = pt;
+  f.r.z = (real*)zout;
+  f.r.z_in = (const real*)zin;
+  f.bar = c->d_bar;
+  f.err = c->d_err;
+  f.NB = fused_rows(c) == 16 ? c->NZh : c->NZ16;
+  f.target = 0;
+  if (c->prof) c->prof->begin(c->stream, K_SEC);
+  if (fused_rows(c) == 16) {
+    if (c->sec3) return fail(SA_ERR_UNSUPPORTED, "fused triple kernel: 16-row blocks");
+    launch_fused_r<real, 16>(c, a, f);
+  } else {
+    launch_fused_r<real, kRow2Rows>(c, a, f);
+  }
+  if (c->prof) c->prof->end(c->stream);
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
 template <typename real>
 int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, void* bout = nullptr) {
   SecArgs<real> a = sec_args<real>(c, mode, t, es);
@@ -3140,9 +3420,12 @@ void pick_row(sa_ctx* c, int B) {
 }
 
 template <typename real>
-int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt = 0) {
+int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt = 0, void* zin = nullptr,
+               void* zout = nullptr) {
   RowArgs<real> a = row_args<real>(c, mode, t, es, G, Gb);
   a.pt = pt;
+  if (zout) a.z = (real*)zout;
+  if (zin) a.z_in = (const real*)zin;
   if (c->prof) c->prof->begin(c->stream, K_ROW);
   // small batch: 16-row workgroups cover the chip; many codewords: 64-row
   // workgroups, 4 waves with deeper per-lane load streams
@@ -3336,8 +3619,7 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const bool sec2 = use_sec2(c, B);
   pick_row(c, B);  // row kernel and its z^2 partial count
   // Ab partials row-block major between the pair / triple kernels and k_row2
-  const int pt = (sec2 && (c->sec3 || c->sec4) && (c->row_kind == 1 || c->row_kind == 4) && c->pt_on)
-                     ? (c->row_kind == 4 ? 16 : kRow2Rows) : 0;
+  const int pt = pt_for(c, B, sec2);
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
   const int G = i8 ? S8 : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
@@ -3359,7 +3641,23 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     k_fill32<<<(int)std::min<size_t>((nw + 255) / 256, 8192), 256, 0, c->stream>>>((uint32_t*)c->d_beta, 0u, nw);
     if ((rc = launch_row<real>(c, B, ROW_INIT0, 0, 0, G, Gb))) return rc;
   }
-  for (int t = 0; t < T; ++t) {
+  const bool fused = !dense && !batched && sec2 && use_fused(c, B, pt);
+  if (fused) {
+    // the fused path: K_0 alone, then K_t = row step t-1 + section step t,
+    // then the row step T-1 alone; z double-buffered (z_t in buffer t & 1)
+    k_fill32<<<1, 256, 0, c->stream>>>(c->d_bar, 0u, (size_t)256);
+    c->bar_seq = 0;
+    void* zb[2] = {c->d_z, c->d_z2};
+    for (int t = 0; t < T; ++t) {
+      void* pin = (t & 1) ? c->d_beta2 : c->d_beta;
+      void* pout = (t & 1) ? c->d_beta : c->d_beta2;
+      if (t == 0) rc = launch_sec2<real>(c, B, t, es, pin, pout, pt);
+      else rc = launch_fused<real>(c, t, es, pin, pout, zb[(t - 1) & 1], zb[t & 1], pt, G, Gb);
+      if (rc) return rc;
+    }
+    if (T > 0 && (rc = launch_row<real>(c, B, ROW_AMP, T - 1, es, G, Gb, pt, zb[(T - 1) & 1], zb[T & 1]))) return rc;
+  }
+  for (int t = 0; t < (fused ? 0 : T); ++t) {
     if (i8) {
       // z -> digit planes -> Az GEMM (into the dense Az buffer, one partial)
       // -> denoiser (+ beta digit planes) -> A beta GEMM (S8 partials)
@@ -3393,6 +3691,11 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     k_beta_final<real><<<dim3((unsigned)std::min<size_t>((LM + 255) / 256, 4096), B), 256, 0, c->stream>>>(
         (real*)c->d_beta, (const real*)c->d_beta2, c->d_iters, LM);
     HIP_TRY(hipGetLastError());
+    if (fused) {
+      k_z_final<real><<<(c->n + 255) / 256, 256, 0, c->stream>>>((real*)c->d_z, (const real*)c->d_z2, c->d_iters,
+                                                                  c->n);
+      HIP_TRY(hipGetLastError());
+    }
   }
   return SA_OK;
 }
@@ -3716,6 +4019,11 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     // (two interleaved A/B rounds).  SPARC_AMP_R16=0: 32-row blocks
     const char* er = getenv("SPARC_AMP_R16");
     c->row16 = !(er && er[0] == '0') && c->pt_on && c->sec4 && c->NZh <= 320;
+  }
+  {
+    // fused row step for one codeword (SPARC_AMP_FUSE=1; see FuseArgs)
+    const char* ef = getenv("SPARC_AMP_FUSE");
+    c->fuse = ef && ef[0] == '1';
   }
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for
@@ -4170,6 +4478,14 @@ int sa_wait(sa_ctx* c) {
   if (check_ctx(c)) return SA_ERR_ARG;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->fuse && c->d_err) {  // a fused launch whose arrival poll gave up: its results are not to be trusted
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) {
+      HIP_TRY(hipMemset(c->d_err, 0, sizeof(int)));
+      return fail(SA_ERR_HIP, "fused row step: the workgroup arrival poll timed out (results discarded)");
+    }
+  }
   return SA_OK;
 }
 
@@ -4542,7 +4858,8 @@ int sa_plan(sa_ctx* c, int B, int64_t* o) {
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
   const bool i8 = use_i8(c, B);
-  o[0] = i8 ? 6 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? 5 : (c->sec4 ? 4 : 1)) : 0)));
+  const bool fused = !dense && !batched && sec2 && use_fused(c, B, pt_for(c, B, sec2));
+  o[0] = i8 ? 6 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? (fused ? 8 : 5) : (c->sec4 ? (fused ? 7 : 4) : 1)) : 0)));
   o[1] = i8 ? i8_splits(c, B) : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
   o[3] = batched ? c->CB : 1;

@@ -1581,7 +1581,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   // z^2 partials held in registers: k_row2 writes ceil(n / 32) (C4 n = 8294:
   // 260, past the 256 of K = 4, whose fallback re-reads them: one more memory
   // round trip before tau), k_row2<16> ceil(n / 16) (C2: 288)
-  ZZParts<real, 5> zz;
+#ifndef SA_ZZK
+#define SA_ZZK 5
+#endif
+  ZZParts<real, SA_ZZK> zz;
   bool dma;
   real last, cl;
   if constexpr (FR > 0) {
@@ -4016,9 +4019,12 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     // 16-row k_row2 blocks for one codeword where the z^2 partials still fit
     // the section kernels' registers (ceil(n / 16) <= 320; C2: 288 workgroups
     // instead of 144, every CU pulls partials): c2 1362-1374 -> 1396 cw/s
-    // (two interleaved A/B rounds).  SPARC_AMP_R16=0: 32-row blocks
+    // (two interleaved A/B rounds).  Binary32 only: in binary64 the 32-row
+    // blocks are faster (c2 fp64 984-988 -> 990-1013 cw/s, two interleaved
+    // rounds, round 3).  SPARC_AMP_R16=0/1 forces 32-/16-row blocks
     const char* er = getenv("SPARC_AMP_R16");
-    c->row16 = !(er && er[0] == '0') && c->pt_on && c->sec4 && c->NZh <= 320;
+    const bool r16 = er ? er[0] != '0' : s == 4;
+    c->row16 = r16 && c->pt_on && c->sec4 && c->NZh <= 320;
   }
   {
     // fused row step for one codeword (SPARC_AMP_FUSE=1; see FuseArgs)

@@ -434,11 +434,16 @@ def test_partial_layouts_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
         monkeypatch.setenv("SPARC_AMP_PT", flag)
         ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
     monkeypatch.delenv("SPARC_AMP_PT")
+    monkeypatch.setenv("SPARC_AMP_R16", "1")  # 16-row blocks where they fit (the binary32 default)
+    ops["16"] = sp.SparcOperator(L, M, n, oord, precision=prec)
     monkeypatch.delenv("SPARC_AMP_R16")
-    ops["16"] = sp.SparcOperator(L, M, n, oord, precision=prec)  # the default: 16-row blocks where they fit
+    dflt = sp.SparcOperator(L, M, n, oord, precision=prec)
     assert ops["1"].plan(1)["section_kernel"] == ("k_sec43" if sec3 == "1" else "k_sec4")
     assert ops["1"].plan(1)["row_kernel"] == "k_row2"
-    assert ops["16"].plan(1)["row_kernel"] == ("k_row2_16" if (n + 15) // 16 <= 320 else "k_row2")
+    fits16 = (n + 15) // 16 <= 320
+    assert ops["16"].plan(1)["row_kernel"] == ("k_row2_16" if fits16 else "k_row2")
+    # binary64 keeps 32-row blocks (faster there)
+    assert dflt.plan(1)["row_kernel"] == ("k_row2_16" if fits16 and prec == "fp32" else "k_row2")
     for t in (1, 4):
         b1, i1 = ops["1"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
         b0, i0 = ops["0"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)

@@ -35,13 +35,26 @@ else:
     names = ["tau+loads", "z->LDS+bar", "wait tables", "gather", "fwht1", "denoise", "fwht2", "ts+bar", "rows",
              "drain"]
 acc = np.zeros(len(order) - 1)
+allw = []
 for rep in range(20):
     op.run(B, T, early_stop=False); op.wait()
-    st = (ct.c_ulonglong * 16)()
+    st = (ct.c_ulonglong * 256)()
     lib.sa_debug_stamps(st)
-    v = np.array([st[i] for i in order], dtype=np.float64)
+    a = np.array(st[:], dtype=np.float64).reshape(16, 16)
+    waves = [w for w in range(16) if a[w, order[0]] > 0 and a[w, order[-1]] > 0]
+    v = a[0, order]
     acc += np.diff(v)
+    allw.append(a[waves][:, order] - a[0, order[0]])  # every wave's stamps from wave 0's start
 acc /= 20
 for nm, c in zip(names, acc):
-    print(f"{nm:12s} {c:9.0f} cycles  {c / acc.sum() * 100:5.1f}%")
+    print(f"{nm:12s} {c:9.0f} cycles  {c / acc.sum() * 100:5.1f}%   (wave 0)")
 print(f"total {acc.sum():.0f} cycles")
+# per-wave view: when each wave reaches the end of each phase (cycles after
+# wave 0's start; mean over the 20 decodes), min / max over the waves
+W = np.mean(np.stack(allw), axis=0)
+print(f"{W.shape[0]} waves stamped; phase ends (cycles from wave 0's start): min / max over waves, and the spread")
+for j, nm in enumerate(names):
+    col = W[:, j + 1]
+    print(f"  end of {nm:12s} min {col.min():9.0f}  max {col.max():9.0f}  spread {col.max() - col.min():8.0f}")
+print("  per wave, end of the last compute phase before the T barrier:",
+      " ".join(f"{x:.0f}" for x in W[:, min(4, W.shape[1] - 1)]))

@@ -9,9 +9,10 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RND = sys.argv[1] if len(sys.argv) > 1 else "r02"
+RND = sys.argv[1] if len(sys.argv) > 1 else "r03"
 # tag -> bench.py load_pmc key (workload_backend_precision_B)
 KEYS = {"c2": "c2_hadamard_fp32_B1", "c4b1": "c4_hadamard_fp32_B1", "c3": "c3_hadamard_fp32_B256",
+        "c4": "c4_hadamard_fp32_B256",
         "dense_l768": "c4_dense_fp32_B1", "c3dense": "c3_dense_fp32_B256"}
 
 

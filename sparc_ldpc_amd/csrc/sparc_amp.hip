@@ -777,6 +777,9 @@ struct SecArgs {
   // G x 128-B block per workgroup)
   int pt;
   int B, NC;  // batched kernel: codewords, codeword chunks of CB
+  // batched kernel: z and the Ab partials codeword-interleaved by chunk,
+  // z [NC][n][CB] and abp [NC][G][n][CB] (16-byte rows, k_rowc), else [B][n] / [B][G][n]
+  int zil;
   real sqrt_n;
 };
 
@@ -798,6 +801,7 @@ struct RowArgs {
   const real* __restrict__ Pb;
   int Pbst;
   int pt;  // Ab partial layout (SecArgs::pt); k_row2 only
+  int Bc;  // k_rowc: codewords of the decode (the last chunk may be partial)
 };
 
 // One workgroup = 4 wavefronts = 4 consecutive sections of one codeword
@@ -1979,6 +1983,20 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   const int region = zslots > W * M * CB ? zslots : W * M * CB;
   real* bbw = zs + region;                   // [W][CB]
 
+  // codeword-interleaved z (a.zil: [NC][n][CB], 16-byte rows): this chunk's
+  // rows straight into LDS by LDS-DMA (1 KB per wave instruction), issued
+  // before anything else; no register staging, no ds_write, no second pass
+  const bool zil = a.zil;
+  if (zil) {
+    const char* zsrc = reinterpret_cast<const char*>(a.z) + (size_t)chunk * n * CB * sizeof(real);
+    const int nbytes = n * CB * (int)sizeof(real);
+    for (int ch = wv; ch * 1024 < nbytes; ch += W) {
+      const int off = ch * 1024 + lane * 16;
+      if (off + 16 <= nbytes)  // rows are 16 bytes: whole rows only
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(zsrc + off),
+                                         (__attribute__((address_space(3))) void*)((char*)zs + ch * 1024), 16, 0, 0);
+    }
+  }
   // ---- every load independent of z in flight together ---------------------
   // the z^2 partials of the CB codewords first: tau waits for these alone
   ZZParts<real, F64 ? 2 : 3> zzc[CB];
@@ -2000,11 +2018,13 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   const real* zc[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) zc[c] = a.z + (size_t)bc[c] * n;
+  if (!zil) {
 #pragma unroll
-  for (int u = 0; u < KZ; ++u) {
-    const int r = u * NT + tid;
+    for (int u = 0; u < KZ; ++u) {
+      const int r = u * NT + tid;
 #pragma unroll
-    for (int c = 0; c < CB; ++c) zr[u][c] = ld_off(zc[c], (unsigned)(r < n ? r : 0) * (unsigned)sizeof(real));
+      for (int c = 0; c < CB; ++c) zr[u][c] = ld_off(zc[c], (unsigned)(r < n ? r : 0) * (unsigned)sizeof(real));
+    }
   }
   // the bank-aware step order (build_invb: sign +1 steps first) or h order
   const bool banked = a.invb != nullptr;
@@ -2049,11 +2069,15 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     any |= live[c];
     tau2[c] = tau * tau;
   }
-  if (!any) return;  // uniform
+  if (!any) {  // uniform
+    if (zil) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write may outlive the workgroup
+    return;
+  }
   STAMP(1);
 
   // ---- z -> LDS interleaved [row][CB] ------------------------------------
-  for (int r0 = 0; r0 < n; r0 += KZ * NT) {
+  if (zil) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed (the barrier: every wave's)
+  for (int r0 = 0; r0 < (zil ? 0 : n); r0 += KZ * NT) {
 #pragma unroll
     for (int u = 0; u < KZ; ++u) {
       const int r = r0 + u * NT + tid;
@@ -2257,9 +2281,17 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
         }
       }
       if (r < n) {
+        if (zil) {  // one 16-byte vector of the CB codewords ([NC][G][n][CB])
+          using V = real __attribute__((ext_vector_type(CB)));
+          V pv;
 #pragma unroll
-        for (int c = 0; c < CB; ++c)
-          if (live[c]) st_part(&a.abp[((size_t)bc[c] * a.G + g) * n + r], acc[c]);
+          for (int c = 0; c < CB; ++c) pv[c] = acc[c];
+          __builtin_nontemporal_store(pv, reinterpret_cast<V*>(a.abp) + ((size_t)chunk * a.G + g) * n + r);
+        } else {
+#pragma unroll
+          for (int c = 0; c < CB; ++c)
+            if (live[c]) st_part(&a.abp[((size_t)bc[c] * a.G + g) * n + r], acc[c]);
+        }
       }
     }
     if (more) {
@@ -2438,6 +2470,134 @@ __global__ void __launch_bounds__(256) k_rowv(RowArgs<real> a) {
   for (int j = 0; j < V; ++j) q += zn[j] * zn[j];
   const real s = wave_sum(q);
   if (lane == 0) a.zzp[(size_t)b * a.NZ + blockIdx.x] = s;
+}
+
+// Row kernel of the codeword-interleaved batched layout (SecArgs::zil): rows
+// of a chunk of CB codewords (CB x sizeof(real) = 16 bytes: binary32 CB = 4,
+// binary64 CB = 2), 128 rows per 256-thread workgroup (lane l: rows l and
+// l + 64), blockIdx.y the chunk.  The four waves split the G Ab partials of
+// those rows (wave w adds its range in order, all its loads in flight
+// together; the four wave sums added in wave order, as k_rowv); the partials
+// are 16-byte vectors [NC][G][n][CB] (pil, behind k_secb) or per codeword
+// [B][G][n] (behind k_sec's SEC_AB, the beta0 start).  Wave 0 then forms the
+// Onsager residual (sparc_ldpc.py:220), stores z [NC][n][CB] as one 16-byte
+// vector per row, and the z^2 partial of each codeword's block.  A stopped
+// codeword keeps its z and z^2 partials.
+template <typename real, int CB>
+__global__ void __launch_bounds__(256) k_rowc(RowArgs<real> a, int pil) {
+  using V = real __attribute__((ext_vector_type(CB)));
+  constexpr int RPL = 2;  // rows per lane
+  __shared__ V red[4][RPL][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int chunk = blockIdx.y, n = a.n;
+  int rr[RPL], ro[RPL];
+  bool in[RPL];
+#pragma unroll
+  for (int k = 0; k < RPL; ++k) {
+    rr[k] = blockIdx.x * 64 * RPL + k * 64 + lane;
+    in[k] = rr[k] < n;
+    ro[k] = in[k] ? rr[k] : 0;
+  }
+  const int B = a.Bc;
+  int bc[CB];
+  bool valid[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const int b = chunk * CB + c;
+    valid[c] = b < B;
+    bc[c] = valid[c] ? b : B - 1;
+  }
+  // wave 0's operands that do not depend on the partials, loaded with them
+  real tau[CB], last[CB], yv[RPL][CB], bbv[CB][2];
+  V zo[RPL] = {};
+  if (wv == 0) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+      tau[c] = 1;
+      last[c] = 0;
+      if (a.mode == ROW_AMP) {
+        tau[c] = ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t);
+        last[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+        const real* bp = a.bbp + (size_t)bc[c] * a.Gb;
+        bbv[c][0] = lane < a.Gb ? bp[lane] : (real)0;
+        bbv[c][1] = lane + 64 < a.Gb ? bp[lane + 64] : (real)0;
+      }
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) yv[k][c] = a.y[(size_t)bc[c] * n + ro[k]];
+    }
+    if (a.mode == ROW_AMP)
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) zo[k] = *reinterpret_cast<const V*>(a.z_in + ((size_t)chunk * n + ro[k]) * CB);
+  }
+  if (a.mode != ROW_INIT0) {
+    const int gq = (a.G + 3) / 4, g0 = wv * gq, g1 = min(a.G, g0 + gq);
+    V acc[RPL] = {};
+    if (pil) {
+      constexpr int U = 8;
+      const V* p = reinterpret_cast<const V*>(a.abp) + (size_t)chunk * a.G * n;
+      for (int gg = g0; gg < g1; gg += U) {
+        V t[RPL][U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int k = 0; k < RPL; ++k)  // dead after this read: streaming loads
+            t[k][u] = __builtin_nontemporal_load(p + (size_t)(gg + u < g1 ? gg + u : g0) * n + ro[k]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (gg + u < g1)
+#pragma unroll
+            for (int k = 0; k < RPL; ++k) acc[k] += t[k][u];
+      }
+    } else {  // the beta0 start only (once per decode): a plain loop
+      for (int g = g0; g < g1; ++g)
+#pragma unroll
+        for (int k = 0; k < RPL; ++k)
+#pragma unroll
+          for (int c = 0; c < CB; ++c) acc[k][c] += a.abp[((size_t)bc[c] * a.G + g) * n + ro[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) red[wv][k][lane] = acc[k];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  real q[CB] = {};
+  bool live[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    live[c] = valid[c] && !(a.mode == ROW_AMP && a.early_stop && tau[c] == last[c]);
+    real ons = 0;
+    const real tau2 = tau[c] * tau[c];
+    if (a.mode == ROW_AMP) {
+      real sacc = 0;
+      sacc += bbv[c][0];
+      sacc += bbv[c][1];
+      const real bb = a.Gb <= 128 ? wave_sum(sacc) : wave_sum_parts(a.bbp + (size_t)bc[c] * a.Gb, a.Gb);
+      ons = a.Pb[(size_t)bc[c] * a.Pbst] - bb / (real)n;
+    }
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      real z;
+      if (a.mode == ROW_INIT0) {
+        z = yv[k][c];
+      } else {
+        const real sv = ((red[0][k][lane][c] + red[1][k][lane][c]) + red[2][k][lane][c]) + red[3][k][lane][c];
+        z = yv[k][c] - sv / a.sqrt_n;
+        if (a.mode == ROW_AMP) z += (zo[k][c] / tau2) * ons;
+      }
+      if (!valid[c]) z = 0;
+      else if (!live[c]) z = zo[k][c];  // a stopped codeword keeps its residual
+      zo[k][c] = z;                     // now the new residual
+      if (in[k]) q[c] += z * z;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RPL; ++k)
+    if (in[k]) *reinterpret_cast<V*>(a.z + ((size_t)chunk * n + rr[k]) * CB) = zo[k];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const real sz = wave_sum(q[c]);
+    if (lane == 0 && live[c]) a.zzp[(size_t)bc[c] * a.NZ + blockIdx.x] = sz;
+  }
 }
 
 // Row kernel for small batches: 32 rows per 512-thread workgroup, so the
@@ -2907,7 +3067,8 @@ struct sa_ctx {
   int* d_err = nullptr;         // set by a fused launch whose arrival poll gave up
   unsigned bar_seq = 0;         // fused launches since the counters were last cleared (host side)
   int NZ4 = 0, NZ2 = 0;  // k_rowv<4> 256-row / k_rowv<2> 128-row blocks
-  int row_kind = 0;    // row kernel of the current decode: 0 k_row, 1 k_row2, 2 k_rowv<4>, 3 k_rowv<2>
+  int row_kind = 0;    // row kernel of the current decode: 0 k_row, 1 k_row2, 2 k_rowv<4>, 3 k_rowv<2>, 4 k_row2<16>, 5 k_rowc
+  bool zil_last = false;  // the last decode left z codeword-interleaved ([NC][n][CB], zil_for)
   int nz_cur = 0;
   size_t sec2_lds = 0;
   std::vector<uint32_t> ordering;
@@ -3098,11 +3259,12 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   if (c->G3 > Gmax) Gmax = c->G3;
   int rc;
   if ((rc = dev_alloc(c, &c->d_y, nB * c->n * s))) return rc;
-  if ((rc = dev_alloc(c, &c->d_z, nB * c->n * s))) return rc;
+  const size_t nBp = (size_t)(nB + 3) / 4 * 4;  // whole chunks of the interleaved batched layout
+  if ((rc = dev_alloc(c, &c->d_z, nBp * c->n * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_beta, nB * LM * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_out, nB * (LM > (size_t)c->n ? LM : (size_t)c->n) * s))) return rc;
   // rows padded to 32: the row-block-major layout of the pair / triple kernels (SecArgs::pt)
-  if ((rc = dev_alloc(c, &c->d_abp, (size_t)nB * Gmax * ((size_t)c->NZ16 * kRow2Rows) * s))) return rc;
+  if ((rc = dev_alloc(c, &c->d_abp, nBp * Gmax * ((size_t)c->NZ16 * kRow2Rows) * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_bbp, (size_t)nB * Gmax * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_zzp, (size_t)nB * c->NZh * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_tau, (size_t)nB * (nT + 1) * s))) return rc;
@@ -3188,7 +3350,7 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   a.T1 = c->Tcap + 1; a.t = t; a.mode = mode; a.early_stop = early_stop;
   a.RS = 1;
   a.pt = 0;
-  a.B = 0; a.NC = 0;
+  a.B = 0; a.NC = 0; a.zil = 0;
   a.cst = c->pb_on ? c->L : 0;
   if (c->pb_on) a.c = (const real*)c->d_cb;
   a.sqrt_n = (real)std::sqrt((double)c->n);
@@ -3209,6 +3371,7 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb
   a.Pb = c->pb_on ? (const real*)c->d_Pb : (const real*)c->d_P1;
   a.Pbst = c->pb_on ? 1 : 0;
   a.pt = 0;
+  a.Bc = 0;
   return a;
 }
 
@@ -3228,12 +3391,15 @@ void launch_sec_e(sa_ctx* c, int B, SecArgs<real> a) {
   if (c->prof) c->prof->end(c->stream);
 }
 
+bool zil_for(const sa_ctx* c, int B);
+
 // Batched section kernel: grid = Gb groups x ceil(B / CB) chunks (1-D, XCD-grouped).
 template <typename real, int E, int CB>
 void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.G = c->Gb;
   a.B = B;
   a.NC = (B + CB - 1) / CB;
+  a.zil = zil_for(c, B) ? 1 : 0;
   if (c->prof) c->prof->begin(c->stream, K_SEC);
   if (c->WB == kWB16)
     PROF_REPS(c) k_secb<real, E, CB, kWB16><<<c->Gb * a.NC, kWB16 * 64, c->secb_lds, c->stream>>>(a);
@@ -3429,7 +3595,16 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
 // Row kernel for B codewords: k_row2 (32-row blocks) while B * ceil(n/64) <
 // 4 CUs, else in binary32 k_rowv<4> (n % 4 == 0) or k_rowv<2> (n even) when
 // their blocks cover the CUs twice, else k_row (64 rows).
+// The batched decode with z and the Ab partials interleaved by codeword chunk
+// (SecArgs::zil, 16-byte rows of CB codewords: binary32 CB = 4, binary64
+// CB = 2), row kernel k_rowc; SPARC_AMP_ZIL=0 keeps the [B][n] layout
+bool zil_for(const sa_ctx* c, int B) {
+  const char* e = getenv("SPARC_AMP_ZIL");
+  return c->backend == SA_BACKEND_HADAMARD && use_batched(c, B) && c->CB * (int)rsz(c) == 16 && !(e && e[0] == '0');
+}
+
 int row_kind_for(const sa_ctx* c, int B) {
+  if (zil_for(c, B)) return 5;
   if ((long long)B * c->NZ < 4LL * c->n_cus) return (c->row16 && B == 1) ? 4 : 1;
   const bool f32 = c->prec == SA_PREC_F32;
   // 16-byte rows: binary32 n % 4 == 0 (256-row blocks) or binary64 n even (128)
@@ -3440,6 +3615,7 @@ int row_kind_for(const sa_ctx* c, int B) {
 int nz_for(const sa_ctx* c, int kind) {
   const bool f32 = c->prec == SA_PREC_F32;
   if (kind == 4) return c->NZh;
+  if (kind == 5) return c->NZ2;  // k_rowc: 128-row blocks
   return kind == 1 ? c->NZ16 : (kind == 2 ? (f32 ? c->NZ4 : c->NZ2) : (kind == 3 ? c->NZ2 : c->NZ));
 }
 void pick_row(sa_ctx* c, int B) {
@@ -3457,7 +3633,13 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt 
   if (c->prof) c->prof->begin(c->stream, K_ROW);
   // small batch: 16-row workgroups cover the chip; many codewords: 64-row
   // workgroups, 4 waves with deeper per-lane load streams
-  if (c->row_kind == 1) {
+  if (c->row_kind == 5 && mode != ROW_ABOUT) {
+    constexpr int CBz = 16 / (int)sizeof(real);  // codewords per 16-byte row
+    a.Bc = B;
+    PROF_REPS(c) k_rowc<real, CBz><<<dim3(c->NZ2, (B + CBz - 1) / CBz), 256, 0, c->stream>>>(a, mode == ROW_AMP ? 1 : 0);
+  } else if (c->row_kind == 5) {  // A beta out of k_sec's [B][G][n] partials (sa_Ab after a batched decode)
+    PROF_REPS(c) k_row<real, 4><<<dim3(c->NZ, B), 4 * 64, 0, c->stream>>>(a);
+  } else if (c->row_kind == 1) {
     PROF_REPS(c) k_row2<real><<<dim3(c->NZ16, B), 512, 0, c->stream>>>(a);
   } else if (c->row_kind == 4) {
     PROF_REPS(c) k_row2<real, 16><<<dim3(c->NZh, B), 512, 0, c->stream>>>(a);
@@ -3646,6 +3828,7 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
   pick_row(c, B);  // row kernel and its z^2 partial count
+  c->zil_last = zil_for(c, B);
   // Ab partials row-block major between the pair / triple kernels and k_row2
   const int pt = pt_for(c, B, sec2);
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
@@ -4590,6 +4773,7 @@ int sa_Az(sa_ctx* c, int B, const double* z, double* out) {
   if (rc) return rc;
   const size_t LM = (size_t)c->L * c->M;
   if ((rc = upload(c, c->d_z, z, (size_t)B * c->n))) return rc;
+  c->zil_last = false;  // d_z holds [B][n] now
   if (c->prec == SA_PREC_F64) {
     rc = seq_az<double>(c, B);
   } else {
@@ -4675,6 +4859,15 @@ int sa_fetch_z(sa_ctx* c, int B, double* z_out) {
   if (B <= 0 || B > c->Bcap) return fail(SA_ERR_ARG, "sa_fetch_z: bad batch");
   HIP_TRY(hipSetDevice(c->device));
   int rc;
+  if (c->zil_last) {  // [NC][n][CB] -> [B][n]
+    const int CB = 16 / (int)rsz(c), NC = (B + CB - 1) / CB;
+    std::vector<double> il((size_t)NC * CB * c->n);
+    if ((rc = download(c, il.data(), c->d_z, il.size()))) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int b = 0; b < B; ++b)
+      for (int r = 0; r < c->n; ++r) z_out[(size_t)b * c->n + r] = il[((size_t)(b / CB) * c->n + r) * CB + b % CB];
+    return SA_OK;
+  }
   if ((rc = download(c, z_out, c->d_z, (size_t)B * c->n))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;

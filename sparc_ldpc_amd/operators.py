@@ -241,7 +241,7 @@ class SparcOperator:
         check(self._lib.sa_plan(self._ctx, int(B), o.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int64))))
         return dict(section_kernel=self.SECTION_KERNELS[int(o[0])], partials=int(o[1]), row_splits=int(o[2]),
                     codewords_per_wg=int(o[3]), zz_partials=int(o[4]), w=int(o[5]),
-                    row_kernel={1: "k_row2", 2: "k_rowv16B", 3: "k_rowv8B", 4: "k_row2_16"}.get(int(o[6]), "k_row"), cus=int(o[7]))
+                    row_kernel={1: "k_row2", 2: "k_rowv16B", 3: "k_rowv8B", 4: "k_row2_16", 5: "k_rowc"}.get(int(o[6]), "k_row"), cus=int(o[7]))
 
     def info(self):
         o = np.zeros(8, dtype=np.int64)

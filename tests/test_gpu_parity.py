@@ -269,15 +269,20 @@ def test_batch_matches_single_and_deterministic(sp, prec, L, M, B):
         assert rel(b6[i], ref) <= TOL[prec]
 
 
-@pytest.mark.parametrize("prec,n,want", [("fp32", 1024, "k_rowv16B"), ("fp32", 1026, "k_rowv8B"),
-                                         ("fp64", 1026, "k_rowv16B"), ("fp32", 1025, "k_row"),
-                                         ("fp64", 1025, "k_row")])
-def test_row_kernel_variants_vs_oracle(sp, prec, n, want):
+@pytest.mark.parametrize("prec,n,want,zil", [("fp32", 1024, "k_rowv16B", "0"), ("fp32", 1026, "k_rowv8B", "0"),
+                                             ("fp64", 1026, "k_rowv16B", "0"), ("fp32", 1025, "k_row", "0"),
+                                             ("fp64", 1025, "k_row", "0"), ("fp32", 1024, "k_rowc", "1"),
+                                             ("fp32", 1025, "k_rowc", "1"), ("fp64", 1026, "k_rowc", "1"),
+                                             ("fp64", 1025, "k_rowc", "1")])
+def test_row_kernel_variants_vs_oracle(sp, prec, n, want, zil, monkeypatch):
     """Every batched row kernel (the Onsager residual of sparc_ldpc.py:220 and
-    the A beta sum of :143-146): k_rowv with 16-byte rows (binary32 n % 4 == 0,
-    binary64 n even), with 8-byte rows (binary32 n even), k_row for odd n; each
-    chosen at B = 128 and checked against the oracle codeword by codeword."""
+    the A beta sum of :143-146): with z and the Ab partials codeword-interleaved
+    (k_rowc, the default where a chunk's row is 16 bytes) and, with
+    SPARC_AMP_ZIL=0, k_rowv with 16-byte rows (binary32 n % 4 == 0, binary64 n
+    even), with 8-byte rows (binary32 n even), k_row for odd n; each chosen at
+    B = 128 and checked against the oracle codeword by codeword."""
     L, M, B, P, T = 128, 256, 128, 2.0, 4
+    monkeypatch.setenv("SPARC_AMP_ZIL", zil)
     op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=prec)
     assert op.plan(B)["row_kernel"] == want, op.plan(B)
     Pl = P / L * np.ones(L)
@@ -540,8 +545,8 @@ def test_amp_init_test(sp, capsys):
 
 def test_c2_batch256_golden(sp):
     """BASELINE configs[2] at its own batch size: 256 codewords of C2 in one
-    decode, which runs the batched section kernel k_secb and the 64-row k_row
-    over the whole grid (the launch shape of the c3 bench line).  Slot 0 holds
+    decode, which runs the batched section kernel k_secb and the
+    codeword-interleaved row kernel k_rowc (the launch shape of the c3 bench line).  Slot 0 holds
     the golden y: t = 1 and the converged estimate against the reference's;
     other slots (seeded reps) against the oracle at fixed t = 2."""
     g = golden("c2.npz")
@@ -549,7 +554,7 @@ def test_c2_batch256_golden(sp):
     B = 256
     op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp32")
     plan = op.plan(B)
-    assert plan["section_kernel"] == "k_secb" and plan["row_kernel"] == "k_rowv16B", plan
+    assert plan["section_kernel"] == "k_secb" and plan["row_kernel"] == "k_rowc", plan  # the c3 bench line's kernels
     Pl = float(g["P"]) / L * np.ones(L)
     oAb, oAz, _ = orc.sparc_transforms(L, M, n)
     sigma = float(g["sigma"])

@@ -1907,7 +1907,7 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
     for (int c = 0; c < CB; ++c) v[c][i] = fma(zz[i][c], sg, v[c][i]);
 }
 
-template <typename real, int E, int CB, int W>
+template <typename real, int E, int CB, int W, bool ZIL = false>
 __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = W * 64;
@@ -1986,7 +1986,10 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // codeword-interleaved z (a.zil: [NC][n][CB], 16-byte rows): this chunk's
   // rows straight into LDS by LDS-DMA (1 KB per wave instruction), issued
   // before anything else; no register staging, no ds_write, no second pass
-  const bool zil = a.zil;
+  // (a template parameter: the two z paths in one kernel cost the binary64
+  // instantiations 32 bytes more scratch)
+  static_assert(!ZIL || CB * sizeof(real) == 16, "codeword-interleaved rows are 16 bytes");
+  constexpr bool zil = ZIL;
   if (zil) {
     const char* zsrc = reinterpret_cast<const char*>(a.z) + (size_t)chunk * n * CB * sizeof(real);
     const int nbytes = n * CB * (int)sizeof(real);
@@ -3401,10 +3404,23 @@ void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.NC = (B + CB - 1) / CB;
   a.zil = zil_for(c, B) ? 1 : 0;
   if (c->prof) c->prof->begin(c->stream, K_SEC);
-  if (c->WB == kWB16)
-    PROF_REPS(c) k_secb<real, E, CB, kWB16><<<c->Gb * a.NC, kWB16 * 64, c->secb_lds, c->stream>>>(a);
-  else
-    PROF_REPS(c) k_secb<real, E, CB, kWB><<<c->Gb * a.NC, kWB * 64, c->secb_lds, c->stream>>>(a);
+  const dim3 grid(c->Gb * a.NC);
+  bool done = false;
+  if constexpr (CB * sizeof(real) == 16) {
+    if (a.zil) {
+      if (c->WB == kWB16)
+        PROF_REPS(c) k_secb<real, E, CB, kWB16, true><<<grid, kWB16 * 64, c->secb_lds, c->stream>>>(a);
+      else
+        PROF_REPS(c) k_secb<real, E, CB, kWB, true><<<grid, kWB * 64, c->secb_lds, c->stream>>>(a);
+      done = true;
+    }
+  }
+  if (!done) {
+    if (c->WB == kWB16)
+      PROF_REPS(c) k_secb<real, E, CB, kWB16><<<grid, kWB16 * 64, c->secb_lds, c->stream>>>(a);
+    else
+      PROF_REPS(c) k_secb<real, E, CB, kWB><<<grid, kWB * 64, c->secb_lds, c->stream>>>(a);
+  }
   if (c->prof) c->prof->end(c->stream);
 }
 
@@ -3597,10 +3613,13 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
 // their blocks cover the CUs twice, else k_row (64 rows).
 // The batched decode with z and the Ab partials interleaved by codeword chunk
 // (SecArgs::zil, 16-byte rows of CB codewords: binary32 CB = 4, binary64
-// CB = 2), row kernel k_rowc; SPARC_AMP_ZIL=0 keeps the [B][n] layout
+// CB = 2), row kernel k_rowc.  Default in binary32 (C3 +1.7 %, C4 +4.7 %);
+// binary64 only with SPARC_AMP_ZIL=1 (its k_secb spills 68 bytes against 36:
+// C3 -1.6 %, the joint decode -1.5 %); SPARC_AMP_ZIL=0 keeps [B][n] always
 bool zil_for(const sa_ctx* c, int B) {
   const char* e = getenv("SPARC_AMP_ZIL");
-  return c->backend == SA_BACKEND_HADAMARD && use_batched(c, B) && c->CB * (int)rsz(c) == 16 && !(e && e[0] == '0');
+  const bool on = e ? e[0] != '0' : c->prec == SA_PREC_F32;
+  return on && c->backend == SA_BACKEND_HADAMARD && use_batched(c, B) && c->CB * (int)rsz(c) == 16;
 }
 
 int row_kind_for(const sa_ctx* c, int B) {
@@ -4258,11 +4277,23 @@ hipError_t lds_attr_all() {
   SA_A((k_secb<real, 8, 1, kWB16>)) SA_A((k_secb<real, 16, 1, kWB16>))
   SA_A((k_secb<real, 1, 2, kWB16>)) SA_A((k_secb<real, 2, 2, kWB16>)) SA_A((k_secb<real, 4, 2, kWB16>))
   SA_A((k_secb<real, 8, 2, kWB16>)) SA_A((k_secb<real, 16, 2, kWB16>))
+  if constexpr (sizeof(real) == 8) {  // codeword-interleaved (16-byte rows: CB = 2)
+    SA_A((k_secb<real, 1, 2, kWB, true>)) SA_A((k_secb<real, 2, 2, kWB, true>)) SA_A((k_secb<real, 4, 2, kWB, true>))
+    SA_A((k_secb<real, 8, 2, kWB, true>)) SA_A((k_secb<real, 16, 2, kWB, true>))
+    SA_A((k_secb<real, 1, 2, kWB16, true>)) SA_A((k_secb<real, 2, 2, kWB16, true>))
+    SA_A((k_secb<real, 4, 2, kWB16, true>)) SA_A((k_secb<real, 8, 2, kWB16, true>))
+    SA_A((k_secb<real, 16, 2, kWB16, true>))
+  }
   if constexpr (sizeof(real) == 4) {
     SA_A((k_secb<real, 1, 4, kWB>)) SA_A((k_secb<real, 2, 4, kWB>)) SA_A((k_secb<real, 4, 4, kWB>))
     SA_A((k_secb<real, 8, 4, kWB>)) SA_A((k_secb<real, 16, 4, kWB>))
     SA_A((k_secb<real, 1, 4, kWB16>)) SA_A((k_secb<real, 2, 4, kWB16>)) SA_A((k_secb<real, 4, 4, kWB16>))
     SA_A((k_secb<real, 8, 4, kWB16>)) SA_A((k_secb<real, 16, 4, kWB16>))
+    SA_A((k_secb<real, 1, 4, kWB, true>)) SA_A((k_secb<real, 2, 4, kWB, true>)) SA_A((k_secb<real, 4, 4, kWB, true>))
+    SA_A((k_secb<real, 8, 4, kWB, true>)) SA_A((k_secb<real, 16, 4, kWB, true>))
+    SA_A((k_secb<real, 1, 4, kWB16, true>)) SA_A((k_secb<real, 2, 4, kWB16, true>))
+    SA_A((k_secb<real, 4, 4, kWB16, true>)) SA_A((k_secb<real, 8, 4, kWB16, true>))
+    SA_A((k_secb<real, 16, 4, kWB16, true>))
   }
 #undef SA_A
   return e;

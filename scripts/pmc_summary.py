@@ -25,7 +25,7 @@ def short(name):
         return "k_gemm_i8_Az"   # three digit planes of z
     if "k_gemm_i8<4>" in name:
         return "k_gemm_i8_Ab"   # four digit planes of beta
-    for k in ("k_secb", "k_sec2", "k_sec43", "k_sec4", "k_sec8", "k_sec", "k_row2", "k_rowv", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide",
+    for k in ("k_secb", "k_sec2", "k_sec43f", "k_sec43", "k_sec4f", "k_sec4", "k_sec8", "k_sec", "k_row2", "k_rowv", "k_rowc", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide",
               "k_gemm_i8", "k_i8_quant", "k_i8_build",
               "k_bp", "k_llr", "k_bp2sp", "k_sp_norm", "k_colsum"):
         if any(p in name for p in (f"::{k}<", f" {k}<", f" {k}(", f"::{k}(")) or name.startswith((f"{k}<", f"{k}(")):

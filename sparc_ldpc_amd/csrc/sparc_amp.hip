@@ -4466,12 +4466,17 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   {
     // k_sec43: three sections per workgroup where pairs overfill the chip
     // (ceil(L/2) > CUs >= ceil(L/3), e.g. L = 768) — one workgroup per CU
-    // instead of two on half of them; SPARC_AMP_SEC3=0/1 forces it off/on
+    // instead of two on half of them; in binary64 also where pairs fill the
+    // chip exactly (L = 2 x CUs, c2): a third fewer 8-byte Ab partials for
+    // k_row2 outweigh the longer section step (c2 fp64 989-997 -> 1026-1027
+    // cw/s, two interleaved A/B rounds, round 3; binary32 at c2: neutral, pairs
+    // kept).  SPARC_AMP_SEC3=0/1 forces it off/on
     const size_t need3 = (((size_t)(n + 1) * s + 15) / 16 * 16) + 6 * (size_t)M * s + 48 * s;
     const char* e3 = getenv("SPARC_AMP_SEC3");
     const int G3 = (L + 2) / 3;
     const bool fits = c->sec4 && backend == SA_BACKEND_HADAMARD && M <= 512 && need3 <= 160 * 1024;
-    const bool want = e3 ? e3[0] == '1' : (c->G2 > c->n_cus && G3 <= c->n_cus);
+    const bool over = c->G2 > c->n_cus || (s == 8 && c->G2 == c->n_cus);
+    const bool want = e3 ? e3[0] == '1' : (over && G3 <= c->n_cus);
     if (fits && want) {
       c->sec3 = true;
       c->G3 = G3;

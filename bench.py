@@ -67,9 +67,16 @@ def sec_bytes(L, M, n, w, B, G, s, kernel="k_sec4"):
     """Algorithmic bytes of one k_sec launch: the bucket and Ab
     tables once (uint16 per slot and per section-row; k_sec43 packs a section
     triple's Ab entries into one uint32 per row), z once per codeword, β read
-    + write, Ab partials written."""
-    fwd = 4 * n * G if kernel == "k_sec43" else 2 * L * n
-    return 2 * L * w + fwd + B * (n * s + 2 * L * M * s + G * n * s)
+    + write, Ab partials written.  k_sec4i / k_sec43i (bucket tables built in
+    LDS from the ordering values) read n ordering values per section instead
+    of the w-entry bucket tables and the Ab table."""
+    if kernel in ("k_sec4i", "k_sec43i"):
+        # bucket tables built in LDS: only the ordering values are read (pairs
+        # one uint32 per row and pair, triples 8 bytes per row and triple)
+        tables = (8 if kernel == "k_sec43i" else 4) * n * G
+    else:
+        tables = 2 * L * w + (4 * n * G if kernel == "k_sec43" else 2 * L * n)
+    return tables + B * (n * s + 2 * L * M * s + G * n * s)
 
 
 def row_bytes(n, B, G, s):

@@ -30,6 +30,10 @@ if op.plan(B)["section_kernel"] in ("k_sec4f", "k_sec43f"):  # the fused kernels
 elif op.plan(B)["section_kernel"] == "k_secb":
     order = [0, 1, 2, 3, 4, 5, 6, 7]
     names = ["loads+tau", "z->LDS+bar", "gather", "fwht+denoise+fwht", "T->LDS+bar", "rows", "drain"]
+elif op.plan(B)["section_kernel"] in ("k_sec4i", "k_sec43i"):  # bucket tables built in LDS (SPARC_AMP_IB=1)
+    order = [0, 1, 2, 10, 13, 3, 4, 5, 6, 7, 8, 9]
+    names = ["tau+loads", "z->LDS+bar", "wait loads", "scatter+bar", "gather", "fwht1", "denoise", "fwht2",
+             "ts+bar", "rows", "drain"]
 else:
     order = [0, 1, 2, 10, 3, 4, 5, 6, 7, 8, 9]
     names = ["tau+loads", "z->LDS+bar", "wait tables", "gather", "fwht1", "denoise", "fwht2", "ts+bar", "rows",

@@ -759,6 +759,10 @@ struct SecArgs {
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
   const uint32_t* __restrict__ fwd3; // [ceil(L/3)][n] a section triple, 10-bit fields k | sign<<9 (M <= 512)
+  // the ordering values themselves (bucket tables built in LDS, SecArgs::ib):
+  // [ceil(L/2)][n] o_0 | o_1 << 16 (pairs), [ceil(L/3)][n] (o_0 | o_1 << 16, o_2) (triples)
+  const uint32_t* __restrict__ fwo2;
+  const uint2* __restrict__ fwo3;
   const real* __restrict__ c;        // [L] sqrt(n * Pl), or [B][L] per codeword (cst = L)
   const real* __restrict__ z;        // [B][n]
   real* __restrict__ beta;           // [B][L*M] previous estimate (read)
@@ -1539,9 +1543,19 @@ __device__ __forceinline__ void grid_arrive_wait(const FuseArgs<real>& f, int ti
 
 // FR > 0: the fused kernel (row step of t-1 on FR-row blocks first, see
 // FuseArgs); FR = 0: the section kernel alone.
-template <typename real, int EQ, int QW, int SPW = 2, int FR = 0>
+// IB: the bucket tables of the workgroup's sections are built in LDS from the
+// ordering values (fwo2 / fwo3: n entries per section, which also give the Ab
+// rows their bucket and sign) instead of loading the w-entry bucket tables
+// and the Ab table: the first memory round trip carries z, the z^2 partials,
+// beta and the ordering values (C2: 18 KB per workgroup instead of 32 + 18 KB
+// over two trips); the tables are filled with the zero slot n while it is in
+// flight, then every row r is written to slot o_l(r) of its sections' tables
+// (ds_write_b16) and the gather reads the tables from LDS.  The same entries
+// as the bucket table in HBM, visited in the same order: bit-identical results.
+template <typename real, int EQ, int QW, int SPW = 2, int FR = 0, bool IB = false>
 __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs<real>* fu = nullptr) {
   static_assert(SPW == 2 || SPW == 3, "sections per workgroup");
+  static_assert(!IB || FR == 0, "the fused kernels load the bucket tables from HBM");
   STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = SPW * QW * 64;
@@ -1569,15 +1583,18 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   real* ts = zs + zslots;          // [SPW][M]   T_l = H_M beta_l
   real* xb = ts + SPW * M;         // [SPW][M]   top-stage exchange, one M per section
   real* red = xb + SPW * M;        // [SPW*QW][4] per-wave max, S, S2, beta^2
+  uint16_t* invs = reinterpret_cast<uint16_t*>(red + SPW * QW * 4);  // IB: [SPW][w] bucket tables (16-B aligned)
 
   real v[EQ];
   real bprev[EQ];
   const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
   real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
-  const uint16_t* il = a.inv + (size_t)lc * a.w + eoff;
+  const uint16_t* il = IB ? invs + sidx * a.w + eoff : a.inv + (size_t)lc * a.w + eoff;
   const uint32_t* fw = (SPW == 2 ? a.fwd2 : a.fwd3) + (size_t)g * n;
   ushort4 tb[KH][NQ];
-  uint32_t f[KR];
+  // Ab-table entries of this thread's rows; IB: the ordering values (triples: two words)
+  using FO = typename std::conditional<IB && SPW == 3, uint2, uint32_t>::type;
+  FO f[KR];
 
   // Load order: z's LDS-DMA first, then the z^2 partials and tau_{t-1}, then
   // the tables, all unconditional (straight-line).  While an LDS-DMA is in
@@ -1624,9 +1641,27 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
     if (!dma) zst.issue(zb, n, tid);
     zz.issue(zzb, a.NZ, lane);
     last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
-    load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
+    if constexpr (IB) {
+      // the ordering values of this thread's rows (one pass: host-checked n <= NT * KR)
+      if constexpr (SPW == 2) {
+        const uint32_t* fo = a.fwo2 + (size_t)g * n;
+#pragma unroll
+        for (int u = 0; u < KR; ++u) { const int r = u * NT + tid; f[u] = fo[r < n ? r : 0]; }
+      } else {
+        const uint2* fo = a.fwo3 + (size_t)g * n;
+#pragma unroll
+        for (int u = 0; u < KR; ++u) { const int r = u * NT + tid; f[u] = fo[r < n ? r : 0]; }
+      }
+    } else {
+      load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
+    }
     load_section<real, EQ>(bl, bprev, lane, Mq);
     cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
+    if constexpr (IB) {  // every slot empty (the zero slot n) while the loads are in flight
+      const uint32_t nn = (uint32_t)n | ((uint32_t)n << 16);
+      uint4* iv = reinterpret_cast<uint4*>(invs);
+      for (int i = tid; i < SPW * a.w / 8; i += NT) iv[i] = make_uint4(nn, nn, nn, nn);
+    }
   }
   const real tau = zz.tau(zzb, a.NZ, n);
   const bool stop = a.early_stop && (tau == last);
@@ -1652,6 +1687,28 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: table loads landed
   STAMP(10);
 #endif
+  if constexpr (IB) {
+    // row r into slot o_l(r) of each of the workgroup's sections (values in
+    // [1, w), distinct per section; a missing section keeps its empty table)
+    const int w = a.w;
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      const int r = u * NT + tid;
+      if (r < n) {
+        if constexpr (SPW == 2) {
+          invs[f[u] & 0xffffu] = (uint16_t)r;
+          if (g * 2 + 1 < a.L) invs[w + (f[u] >> 16)] = (uint16_t)r;
+        } else {
+          invs[f[u].x & 0xffffu] = (uint16_t)r;
+          if (g * 3 + 1 < a.L) invs[w + (f[u].x >> 16)] = (uint16_t)r;
+          if (g * 3 + 2 < a.L) invs[2 * w + f[u].y] = (uint16_t)r;
+        }
+      }
+    }
+    __syncthreads();
+    STAMP(13);
+    load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // from LDS
+  }
 
 #pragma unroll
   for (int i = 0; i < EQ; ++i) v[i] = 0;
@@ -1673,7 +1730,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   // flight, instead of adding their bytes (C2 18 KB, C4 33 KB per workgroup)
   // to the first memory round trip, which every wave waits for (C4 single
   // codeword 860 -> 894 cw/s, c2 1378 -> 1394; `k_sec43` 11.0 -> 10.7 us)
-  if constexpr (FR == 0) {
+  if constexpr (FR == 0 && !IB) {
 #pragma unroll
     for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
       const int r = u * NT + tid;
@@ -1743,25 +1800,43 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   const size_t npad = (size_t)((n + (1 << psh) - 1) >> psh) << psh;
   real* abq = a.abp + (size_t)b * a.G * npad + ((size_t)g << psh);  // pt: + (r >> psh) * G * R + (r & (R - 1))
   for (int r0 = 0; r0 < n; r0 += NT * KR) {
-    if (r0 > 0) {  // n > NT * KR only
+    if constexpr (!IB) {
+      if (r0 > 0) {  // n > NT * KR only
 #pragma unroll
-      for (int u = 0; u < KR; ++u) {
-        const int r = r0 + u * NT + tid;
-        f[u] = fw[r < n ? r : 0];
+        for (int u = 0; u < KR; ++u) {
+          const int r = r0 + u * NT + tid;
+          f[u] = fw[r < n ? r : 0];
+        }
       }
     }
 #pragma unroll
     for (int u = 0; u < KR; ++u) {
       const int r = r0 + u * NT + tid;
       if (r < n) {
-        const uint32_t e = f[u];
         real t;
-        if constexpr (SPW == 2) {
+        if constexpr (IB) {
+          // bucket o & (M-1), sign parity(o >> log2 M): the Ab-table entry of the ordering value
+          const int lgM = 31 - __clz(M);
+          auto term = [&](uint32_t o, int sec) {
+            const real v0 = ts[sec * M + (o & (uint32_t)(M - 1))];
+            return (__popc(o >> lgM) & 1) ? -v0 : v0;
+          };
+          if constexpr (SPW == 2) {
+            t = term(f[u] & 0xffffu, 0);
+            t += term(f[u] >> 16, 1);
+          } else {
+            t = term(f[u].x & 0xffffu, 0);
+            t += term(f[u].x >> 16, 1);
+            t += term(f[u].y, 2);
+          }
+        } else if constexpr (SPW == 2) {
+          const uint32_t e = f[u];
           const real v0 = ts[e & 0x7fffu];
           const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
           t = (e & 0x8000u) ? -v0 : v0;
           t += (e & 0x80000000u) ? -v1 : v1;
         } else {
+          const uint32_t e = f[u];
           const real v0 = ts[e & 0x1ffu];
           const real v1 = ts[M + ((e >> 10) & 0x1ffu)];
           const real v2 = ts[2 * M + ((e >> 20) & 0x1ffu)];
@@ -1781,12 +1856,12 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
 #endif
 }
 
-template <typename real, int E4>
-__global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) { secq_body<real, E4, 4>(a); }
+template <typename real, int E4, bool IB = false>
+__global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) { secq_body<real, E4, 4, 2, 0, IB>(a); }
 // Three sections per workgroup (12 waves): L = 3 x CUs (L = 768 on 256 CUs)
 // puts one workgroup on every CU where pairs leave half the CUs with two.
-template <typename real, int E4>
-__global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real, E4, 4, 3>(a); }
+template <typename real, int E4, bool IB = false>
+__global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real, E4, 4, 3, 0, IB>(a); }
 // The fused kernels (row step of t-1, hand-off, section step of t)
 template <typename real, int E4, int FR>
 __global__ void __launch_bounds__(512) k_sec4f(SecArgs<real> a, FuseArgs<real> f) {
@@ -3061,6 +3136,13 @@ struct sa_ctx {
   bool pt_on = false;  // row-block-major Ab partials between k_sec4 / k_sec43 and k_row2 (SecArgs::pt)
   bool sec4 = false;   // k_sec4 (4 waves per section) fits and is chosen
   size_t sec4_lds = 0;
+  // bucket tables built in LDS from the ordering values (k_sec4 / k_sec43 <IB>):
+  // the section kernel loads fwo2 / fwo3 (n entries per section) instead of the
+  // w-entry bucket table plus the Ab table; sec4_lds / sec3_lds include the
+  // LDS image of the bucket tables
+  bool ib = false;
+  uint32_t* d_fwo2 = nullptr;
+  uint2* d_fwo3 = nullptr;
   int NZ16 = 0;        // k_row2 32-row blocks; nz_cur = z^2 partial count of the current decode
   int NZh = 0;         // k_row2 16-row blocks (row16)
   bool row16 = false;  // k_row2<16> after k_sec4 (row-block-major partials, NZh <= 320)
@@ -3346,6 +3428,7 @@ template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
   a.inv = c->d_inv; a.invb = c->d_invb; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
+  a.fwo2 = c->d_fwo2; a.fwo3 = c->d_fwo3;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
@@ -3478,10 +3561,24 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout, int pt =
   dim3 grid(a.G, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
   if (c->sec3) {
-    switch (c->M / 256) {
-      case 1: PROF_REPS(c) k_sec43<real, 1><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
-      case 2: PROF_REPS(c) k_sec43<real, 2><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
+    const size_t lds3 = c->sec3_lds + (c->ib ? 3 * (size_t)c->w * 2 : 0);
+    switch (c->M / 256 + (c->ib ? 2 : 0)) {
+      case 1: PROF_REPS(c) k_sec43<real, 1><<<grid, 768, lds3, c->stream>>>(a); break;
+      case 2: PROF_REPS(c) k_sec43<real, 2><<<grid, 768, lds3, c->stream>>>(a); break;
+      case 3: PROF_REPS(c) k_sec43<real, 1, true><<<grid, 768, lds3, c->stream>>>(a); break;
+      case 4: PROF_REPS(c) k_sec43<real, 2, true><<<grid, 768, lds3, c->stream>>>(a); break;
       default: return fail(SA_ERR_UNSUPPORTED, "k_sec43: M");
+    }
+    if (c->prof) c->prof->end(c->stream);
+    HIP_TRY(hipGetLastError());
+    return SA_OK;
+  }
+  if (c->sec4 && c->ib) {
+    const size_t lds4 = c->sec4_lds + 2 * (size_t)c->w * 2;
+    switch (c->M / 256) {
+      case 1: PROF_REPS(c) k_sec4<real, 1, true><<<grid, 512, lds4, c->stream>>>(a); break;
+      case 2: PROF_REPS(c) k_sec4<real, 2, true><<<grid, 512, lds4, c->stream>>>(a); break;
+      default: return fail(SA_ERR_UNSUPPORTED, "k_sec4<IB>: M");
     }
     if (c->prof) c->prof->end(c->stream);
     HIP_TRY(hipGetLastError());
@@ -4064,6 +4161,9 @@ int build_tables(sa_ctx* c) {
   std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);  // [G][n][4]; missing sections -> (k 0, +)
   std::vector<uint32_t> fwd2((size_t)((L + 1) / 2) * n, 0);  // [L/2][n] section pairs
   std::vector<uint32_t> fwd3(c->sec3 ? (size_t)c->G3 * n : 0, 0);  // [L/3][n] section triples
+  // ordering values for the in-LDS bucket tables (c->ib): pairs o0 | o1 << 16, triples (o0 | o1 << 16, o2)
+  std::vector<uint32_t> fwo2(c->ib && !c->sec3 ? (size_t)((L + 1) / 2) * n : 0, 0);
+  std::vector<uint32_t> fwo3(c->ib && c->sec3 ? (size_t)c->G3 * n * 2 : 0, 0);
   for (int l = 0; l < L; ++l) {
     const uint32_t* o = c->ordering.data() + (size_t)l * n;
     uint16_t* il = inv.data() + (size_t)l * w;
@@ -4081,6 +4181,8 @@ int build_tables(sa_ctx* c) {
       fwd2[(size_t)(l / 2) * n + r] |= (uint32_t)e << (16 * (l & 1));
       if (c->sec3)  // M <= 512: k in 9 bits, the sign in bit 9 of a 10-bit field
         fwd3[(size_t)(l / 3) * n + r] |= (uint32_t)((e & 0x1ffu) | ((e >> 15) << 9)) << (10 * (l % 3));
+      if (!fwo2.empty()) fwo2[(size_t)(l / 2) * n + r] |= v << (16 * (l & 1));
+      if (!fwo3.empty()) fwo3[((size_t)(l / 3) * n + r) * 2 + (l % 3 == 2)] |= v << (l % 3 == 1 ? 16 : 0);
     }
   }
   int rc;
@@ -4088,6 +4190,8 @@ int build_tables(sa_ctx* c) {
   if ((rc = dev_alloc(c, (void**)&c->d_fwd, fwd.size() * 2))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_fwd2, fwd2.size() * 4))) return rc;
   if (c->sec3 && (rc = dev_alloc(c, (void**)&c->d_fwd3, fwd3.size() * 4))) return rc;
+  if (!fwo2.empty() && (rc = dev_alloc(c, (void**)&c->d_fwo2, fwo2.size() * 4))) return rc;
+  if (!fwo3.empty() && (rc = dev_alloc(c, (void**)&c->d_fwo3, fwo3.size() * 4))) return rc;
   // On the context's (non-blocking) stream and waited for: a pageable
   // hipMemcpy may return once the data is staged, before the DMA lands, and
   // the null stream does not order the kernels of a non-blocking stream.
@@ -4096,6 +4200,10 @@ int build_tables(sa_ctx* c) {
   HIP_TRY(hipMemcpyAsync(c->d_fwd2, fwd2.data(), fwd2.size() * 4, hipMemcpyHostToDevice, c->stream));
   if (c->sec3)
     HIP_TRY(hipMemcpyAsync(c->d_fwd3, fwd3.data(), fwd3.size() * 4, hipMemcpyHostToDevice, c->stream));
+  if (!fwo2.empty())
+    HIP_TRY(hipMemcpyAsync(c->d_fwo2, fwo2.data(), fwo2.size() * 4, hipMemcpyHostToDevice, c->stream));
+  if (!fwo3.empty())
+    HIP_TRY(hipMemcpyAsync(c->d_fwo3, fwo3.data(), fwo3.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
@@ -4286,6 +4394,7 @@ hipError_t lds_attr_all() {
   SA_A((k_sec4<real, 1>)) SA_A((k_sec4<real, 2>)) SA_A((k_sec4<real, 4>)) SA_A((k_sec4<real, 8>))
   SA_A((k_sec4<real, 16>))
   SA_A((k_sec43<real, 1>)) SA_A((k_sec43<real, 2>))
+  SA_A((k_sec4<real, 1, true>)) SA_A((k_sec4<real, 2, true>)) SA_A((k_sec43<real, 1, true>)) SA_A((k_sec43<real, 2, true>))
   SA_A((k_secb<real, 1, 1, kWB>)) SA_A((k_secb<real, 2, 1, kWB>)) SA_A((k_secb<real, 4, 1, kWB>))
   SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
   SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
@@ -4482,6 +4591,20 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       c->G3 = G3;
       c->sec3_lds = need3;
     }
+  }
+  {
+    // bucket tables built in LDS (secq_body<IB>) for the pair / triple
+    // kernels: M 256 or 512 (the instantiated widths), every row in one pass
+    // of the thread's Ab-table registers (pairs n <= 4608, triples n <= 8448),
+    // ordering values in 16 bits (w <= 65536) and the tables' LDS image
+    // (SPW x w x 2 B) beside the kernel's own.  SPARC_AMP_IB=0/1 forces it off/on
+    const char* eib = getenv("SPARC_AMP_IB");
+    const bool want = eib ? eib[0] == '1' : false;
+    const int spw = c->sec3 ? 3 : 2;
+    const size_t lds = (c->sec3 ? c->sec3_lds : c->sec4_lds) + (size_t)spw * c->w * 2;
+    const bool fits = backend == SA_BACKEND_HADAMARD && (c->sec3 || c->sec4) && (M == 256 || M == 512) &&
+                      n <= (c->sec3 ? 8448 : 4608) && c->w <= 65536 && lds <= 160 * 1024;
+    c->ib = want && fits;
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -4790,6 +4913,8 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_fwd);
   dev_free(c->d_fwd2);
   dev_free(c->d_fwd3);
+  dev_free(c->d_fwo2);
+  dev_free(c->d_fwo3);
   dev_free(c->d_A);
   dev_free(c->d_A8); dev_free(c->d_AT8); dev_free(c->d_zq); dev_free(c->d_bq);
   dev_free(c->d_zsc); dev_free(c->d_bsc0); dev_free(c->d_bfix);
@@ -5281,7 +5406,9 @@ int sa_plan(sa_ctx* c, int B, int64_t* o) {
   const bool sec2 = use_sec2(c, B);
   const bool i8 = use_i8(c, B);
   const bool fused = !dense && !batched && sec2 && use_fused(c, B, pt_for(c, B, sec2));
-  o[0] = i8 ? 6 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? (fused ? 8 : 5) : (c->sec4 ? (fused ? 7 : 4) : 1)) : 0)));
+  o[0] = i8 ? 6 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? (fused ? 8 : (c->ib ? 10 : 5))
+                                                             : (c->sec4 ? (fused ? 7 : (c->ib ? 9 : 4)) : 1))
+                                                  : 0)));
   o[1] = i8 ? i8_splits(c, B) : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
   o[3] = batched ? c->CB : 1;

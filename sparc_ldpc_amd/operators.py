@@ -227,7 +227,9 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, None, it.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return it
 
-    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43", "dense_mfma", "k_sec4f", "k_sec43f")
+    # k_sec4i / k_sec43i: the pair / triple kernels with their bucket tables built in LDS (SecArgs::ib)
+    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43", "dense_mfma", "k_sec4f", "k_sec43f",
+                       "k_sec4i", "k_sec43i")
 
     def fetch_z(self, B):
         """Residual z after the last decode's final iteration, (B, n)."""

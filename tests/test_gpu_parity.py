@@ -465,6 +465,42 @@ def test_partial_layouts_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
         assert rel(b16[0], ref) <= TOL[prec], t
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+@pytest.mark.parametrize("L,M,n,sec3", [(512, 512, 4608, "0"), (257, 256, 2284, "0"), (258, 512, 2580, "1"),
+                                        (300, 512, 6000, "1"), (768, 512, 8294, "1")])
+def test_lds_bucket_tables_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
+    """Bucket tables built in LDS from the ordering values (SPARC_AMP_IB=1:
+    k_sec4i / k_sec43i) hold the same entries as the bucket table in HBM and
+    are gathered in the same order: decodes bit-identical to the HBM-table
+    kernels (incl. a missing second / third section and n past one row pass
+    of the pair kernel), with and without the early stop; and against the
+    oracle."""
+    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
+    Pl = 2.0 / L * np.ones(L)
+    y = orc.rep_inputs(L, M, n, Pl, 0.9, oAb, 91)[1].reshape(-1)
+    monkeypatch.setenv("SPARC_AMP_SEC3", sec3)
+    ops = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SPARC_AMP_IB", flag)
+        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
+    monkeypatch.delenv("SPARC_AMP_IB")
+    base = "k_sec43" if sec3 == "1" else "k_sec4"
+    fits = (M == 256 or M == 512) and n <= (8448 if sec3 == "1" else 4608)
+    if prec == "fp64" and sec3 == "1" and n > 6000:
+        fits = False  # binary64 z (66 KB) + three 32 KB tables exceed the LDS
+    assert ops["0"].plan(1)["section_kernel"] == base
+    assert ops["1"].plan(1)["section_kernel"] == (base + "i" if fits else base)
+    for t in (1, 3):
+        b1, i1 = ops["1"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+        b0, i0 = ops["0"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
+        assert np.array_equal(b1, b0) and np.array_equal(i1, i0), t
+        ref, _ = orc.amp_test(y, 0, Pl, L, M, t, oAb, oAz)
+        assert rel(b1[0], ref) <= TOL[prec], t
+    b1, i1 = ops["1"].amp_batch(y.reshape(1, -1), Pl, 25)
+    b0, i0 = ops["0"].amp_batch(y.reshape(1, -1), Pl, 25)
+    assert np.array_equal(b1, b0) and np.array_equal(i1, i0)
+
+
 def test_c4_single_uses_triples(sp):
     """L=768 M=512 R=5/6 (n=8294) single codeword: the triple kernel is the
     default where pairs overfill the chip (ceil(L/2) > CUs >= ceil(L/3))."""

@@ -916,6 +916,36 @@ template <typename real, int E, int KH>
 __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
                                                const ushort4 (&tb)[KH][(E + 3) / 4], real (&v)[E]) {
   constexpr int Q = E < 4 ? E : 4;
+  if constexpr (KH * E <= 64) {
+    if (h0 + KH <= nhi) {  // uniform: every step of the block exists
+      // all KH x E LDS reads issued before the first add: the guarded per-step
+      // form below made the compiler wait for each step's reads before the
+      // next step's (lgkmcnt(0) per step: 16 LDS latencies in a row at c2)
+      real zz[KH][E];
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh)
+#pragma unroll
+        for (int i = 0; i < E; i += Q) {
+          const ushort4 r4 = tb[hh][i / Q];
+          const unsigned short rr[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+#ifdef SA_DIAG_GATHER_FAKE  // diagnostic (stamps builds): conflict-free consecutive rows, wrong results
+            zz[hh][i + q] = zs[((threadIdx.x & 63) * Q + q + (rr[q] & 1)) & 4095];
+#else
+            zz[hh][i + q] = zs[rr[q]];
+#endif
+          }
+        }
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh) {
+        const bool neg = __popc(h0 + hh) & 1;  // the same adds in the same (h) order as below
+#pragma unroll
+        for (int i = 0; i < E; ++i) v[i] += neg ? -zz[hh][i] : zz[hh][i];
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int hh = 0; hh < KH; ++hh) {
     if (h0 + hh < nhi) {
@@ -926,7 +956,11 @@ __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
         const unsigned short rr[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
+#ifdef SA_DIAG_GATHER_FAKE  // diagnostic (stamps builds): conflict-free consecutive rows, wrong results
+          const real zz = zs[((threadIdx.x & 63) * Q + q + (rr[q] & 1)) & 4095];
+#else
           const real zz = zs[rr[q]];
+#endif
           v[i + q] += neg ? -zz : zz;
         }
       }
@@ -1799,6 +1833,13 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   const int psh = a.pt == 16 ? 4 : 5;  // pt: rows per block 16 / 32
   const size_t npad = (size_t)((n + (1 << psh) - 1) >> psh) << psh;
   real* abq = a.abp + (size_t)b * a.G * npad + ((size_t)g << psh);  // pt: + (r >> psh) * G * R + (r & (R - 1))
+  real* const sbase = a.pt ? abq : abp;
+  const int sh = a.pt ? psh : 31;
+  const size_t gstride = (size_t)a.G << sh;
+  const int smask = (int)((1u << sh) - 1u);
+#ifdef SA_DIAG_ROWS_NOSTORE
+  real diag_sink = 0;
+#endif
   for (int r0 = 0; r0 < n; r0 += NT * KR) {
     if constexpr (!IB) {
       if (r0 > 0) {  // n > NT * KR only
@@ -1809,46 +1850,66 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
         }
       }
     }
-#pragma unroll
-    for (int u = 0; u < KR; ++u) {
-      const int r = r0 + u * NT + tid;
-      if (r < n) {
-        real t;
-        if constexpr (IB) {
-          // bucket o & (M-1), sign parity(o >> log2 M): the Ab-table entry of the ordering value
-          const int lgM = 31 - __clz(M);
-          auto term = [&](uint32_t o, int sec) {
-            const real v0 = ts[sec * M + (o & (uint32_t)(M - 1))];
-            return (__popc(o >> lgM) & 1) ? -v0 : v0;
-          };
-          if constexpr (SPW == 2) {
-            t = term(f[u] & 0xffffu, 0);
-            t += term(f[u] >> 16, 1);
-          } else {
-            t = term(f[u].x & 0xffffu, 0);
-            t += term(f[u].x >> 16, 1);
-            t += term(f[u].y, 2);
-          }
-        } else if constexpr (SPW == 2) {
-          const uint32_t e = f[u];
-          const real v0 = ts[e & 0x7fffu];
-          const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
-          t = (e & 0x8000u) ? -v0 : v0;
-          t += (e & 0x80000000u) ? -v1 : v1;
+    // row r's term of the pair (triple) and its store
+    auto row = [&](int u, int r) {
+      real t;
+      if constexpr (IB) {
+        // bucket o & (M-1), sign parity(o >> log2 M): the Ab-table entry of the ordering value
+        const int lgM = 31 - __clz(M);
+        auto term = [&](uint32_t o, int sec) {
+          const real v0 = ts[sec * M + (o & (uint32_t)(M - 1))];
+          return (__popc(o >> lgM) & 1) ? -v0 : v0;
+        };
+        if constexpr (SPW == 2) {
+          t = term(f[u] & 0xffffu, 0);
+          t += term(f[u] >> 16, 1);
         } else {
-          const uint32_t e = f[u];
-          const real v0 = ts[e & 0x1ffu];
-          const real v1 = ts[M + ((e >> 10) & 0x1ffu)];
-          const real v2 = ts[2 * M + ((e >> 20) & 0x1ffu)];
-          t = (e & 0x200u) ? -v0 : v0;
-          t += (e & 0x80000u) ? -v1 : v1;
-          t += (e & 0x20000000u) ? -v2 : v2;
+          t = term(f[u].x & 0xffffu, 0);
+          t += term(f[u].x >> 16, 1);
+          t += term(f[u].y, 2);
         }
-        if (a.pt) st_part(&abq[(size_t)(r >> psh) * ((size_t)a.G << psh) + (r & ((1 << psh) - 1))], t);
-        else st_part(&abp[r], t);
+      } else if constexpr (SPW == 2) {
+        const uint32_t e = f[u];
+#ifdef SA_DIAG_ROWS_NOLDS  // diagnostic (stamps builds): no LDS reads in the Ab rows, wrong results
+        const real v0 = (real)(e & 0xffu), v1 = (real)((e >> 16) & 0xffu);
+#else
+        const real v0 = ts[e & 0x7fffu];
+        const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
+#endif
+        t = (e & 0x8000u) ? -v0 : v0;
+        t += (e & 0x80000000u) ? -v1 : v1;
+      } else {
+        const uint32_t e = f[u];
+        const real v0 = ts[e & 0x1ffu];
+        const real v1 = ts[M + ((e >> 10) & 0x1ffu)];
+        const real v2 = ts[2 * M + ((e >> 20) & 0x1ffu)];
+        t = (e & 0x200u) ? -v0 : v0;
+        t += (e & 0x80000u) ? -v1 : v1;
+        t += (e & 0x20000000u) ? -v2 : v2;
+      }
+#ifdef SA_DIAG_ROWS_NOSTORE  // diagnostic (stamps builds): one store per thread instead of one per row
+      diag_sink += t;
+#else
+      // one branch-free store for both layouts: [G][n] is the row-block form with sh = 31
+      st_part(&sbase[(size_t)(r >> sh) * gstride + (r & smask)], t);
+#endif
+    };
+    if (r0 + NT * KR <= n) {
+      // uniform: every row of the pass exists; no per-row branch, so the
+      // LDS reads of several rows are in flight together (c2: n = 9 x 512)
+#pragma unroll
+      for (int u = 0; u < KR; ++u) row(u, r0 + u * NT + tid);
+    } else {
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        const int r = r0 + u * NT + tid;
+        if (r < n) row(u, r);
       }
     }
   }
+#ifdef SA_DIAG_ROWS_NOSTORE
+  st_part(&abp[tid], diag_sink);
+#endif
 #ifdef SA_STAMPS
   STAMP(8);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

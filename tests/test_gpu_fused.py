@@ -66,6 +66,8 @@ def test_fused_bit_identical_to_two_kernel_path(sp, prec, early_stop, case):
     y = np.asarray(g[ykey], dtype=np.float64).reshape(-1)
     fused = _op(sp, L, M, n, prec, True)
     plain = _op(sp, L, M, n, prec, False)
+    if prec == "fp64" and kname == "k_sec4f" and plain.plan(1)["section_kernel"] == "k_sec43":
+        kname = "k_sec43f"  # binary64 runs L = 2 x CUs (c2 on 256 CUs) on the triple kernel
     assert fused.plan(1)["section_kernel"] == kname
     assert plain.plan(1)["section_kernel"] == kname[:-1]
     ref = _decode(plain, y, Pl, T, early_stop)[0]

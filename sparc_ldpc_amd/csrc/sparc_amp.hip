@@ -937,11 +937,37 @@ __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
 #endif
           }
         }
+      if constexpr (KH * E > 16) {
 #pragma unroll
-      for (int hh = 0; hh < KH; ++hh) {
-        const bool neg = __popc(h0 + hh) & 1;  // the same adds in the same (h) order as below
+        for (int hh = 0; hh < KH; ++hh) {
+          const bool neg = __popc(h0 + hh) & 1;  // the same adds in the same (h) order as below
 #pragma unroll
-        for (int i = 0; i < E; ++i) v[i] += neg ? -zz[hh][i] : zz[hh][i];
+          for (int i = 0; i < E; ++i) v[i] += neg ? -zz[hh][i] : zz[hh][i];
+        }
+      } else {
+#pragma unroll
+        for (int hh = 0; hh < KH; ++hh) {
+          // the same sums in the same (h) order: fma(z, -1, v) is v - z
+          // rounded once, as v + (-z) is; one VALU op per element
+          const real sg = (__popc(h0 + hh) & 1) ? (real)-1 : (real)1;
+#pragma unroll
+          for (int i = 0; i < E; ++i) v[i] = fma(zz[hh][i], sg, v[i]);
+        }
+        // blocks of at most 16 reads (C4 triples: 8 h-steps x 2): software
+        // pipeline, 14 reads in flight up front, then one read per fma (the
+        // default schedule issued 8, waited them all out, then 8 more): C4
+        // single codeword +1.5-2.4 %.  For the 32 reads of a c2 block the
+        // default schedule and the select + add form measured faster (c2
+        // -0.9 % with the pipeline; -1.5-4 % with the fma form and the
+        // precomputed partial-store addresses of the Ab rows)
+        constexpr int kPre = KH * E < 14 ? KH * E : 14;
+        __builtin_amdgcn_sched_group_barrier(0x100, kPre, 0);  // DS read
+#pragma unroll
+        for (int k = kPre; k < KH * E; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);    // VALU
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);    // DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, kPre, 0);
       }
       return;
     }
@@ -1596,7 +1622,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   // bucket h-steps whose table loads are in flight together: triples take 8
   // (C4, 32 h-steps: half the first round trip's table bytes, the rest lands
   // during the gather; 961 -> 996 cw/s), pairs 16 (c2: all 16 up front; 8 neutral)
-  constexpr int KH = EQ >= 8 ? 4 : (SPW == 3 ? 8 : 16);
+#ifndef SA_KH3
+#define SA_KH3 8
+#endif
+  constexpr int KH = EQ >= 8 ? 4 : (SPW == 3 ? SA_KH3 : 16);
   constexpr int NQ = (EQ + 3) / 4;
   // rows per thread per pass, all Ab-table loads issued with the first loads: n <= 4608 (pairs,
   // C2) / 8448 (triples, C4 n = 8294) in one pass (a second pass reloads the table mid-phase:
@@ -1837,6 +1866,8 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   const int sh = a.pt ? psh : 31;
   const size_t gstride = (size_t)a.G << sh;
   const int smask = (int)((1u << sh) - 1u);
+  static_assert(NT % 32 == 0, "a pass of rows is a whole number of row blocks");
+  const size_t ustep = sh < 31 ? (size_t)(NT >> sh) * gstride : (size_t)NT;
 #ifdef SA_DIAG_ROWS_NOSTORE
   real diag_sink = 0;
 #endif
@@ -1850,6 +1881,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
         }
       }
     }
+    real* const pbase = sbase + (size_t)((r0 + tid) >> sh) * gstride + ((r0 + tid) & smask);
     // row r's term of the pair (triple) and its store
     auto row = [&](int u, int r) {
       real t;
@@ -1890,8 +1922,12 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
 #ifdef SA_DIAG_ROWS_NOSTORE  // diagnostic (stamps builds): one store per thread instead of one per row
       diag_sink += t;
 #else
-      // one branch-free store for both layouts: [G][n] is the row-block form with sh = 31
-      st_part(&sbase[(size_t)(r >> sh) * gstride + (r & smask)], t);
+      // one branch-free store for both layouts ([G][n] is the row-block form
+      // with sh = 31); triples: row r0 + tid + u NT at pbase + u ustep (NT is
+      // a whole number of 16- / 32-row blocks; pairs measured faster with the
+      // address from r)
+      if constexpr (SPW == 3) st_part(pbase + u * ustep, t);
+      else st_part(&sbase[(size_t)(r >> sh) * gstride + (r & smask)], t);
 #endif
     };
     if (r0 + NT * KR <= n) {

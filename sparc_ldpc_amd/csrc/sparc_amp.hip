@@ -2819,6 +2819,19 @@ __global__ void __launch_bounds__(NT) k_row2(RowArgs<real> a) {
                          : a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
     real acc = 0;
     constexpr int U = 256 / NG;  // G = 256 (C2, C4): every load of a thread in one pass
+    if (R == 16 && a.G == NG * U) {
+      // 16-row blocks (always row-block major) with exactly NG x U partials:
+      // constant strides from the block base, no bounds, 32-bit offsets (the
+      // general form spent ~40 VALU ops of 64-bit address math before the
+      // first load); the same loads and sums in the same order
+      const real* pb = a.abp + (size_t)b * a.G * ((size_t)gridDim.x * R) + (size_t)blockIdx.x * a.G * R;
+      real t[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        t[u] = ld_off(pb, (unsigned)(((pg + NG * u) * R + rl) * (int)sizeof(real)));
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += t[u];
+    } else
     for (int g0 = pg; g0 < a.G; g0 += NG * U) {
       real t[U];
 #pragma unroll

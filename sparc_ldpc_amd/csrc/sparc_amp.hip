@@ -2819,8 +2819,10 @@ __global__ void __launch_bounds__(NT) k_row2(RowArgs<real> a) {
                          : a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
     real acc = 0;
     constexpr int U = 256 / NG;  // G = 256 (C2, C4): every load of a thread in one pass
-    if (R == 16 && a.G == NG * U) {
-      // 16-row blocks (always row-block major) with exactly NG x U partials:
+    if ((R == 16 || (a.pt && sizeof(real) == 4)) && a.G == NG * U) {
+      // row-block-major partials (16-row blocks always are) with exactly NG x U
+      // partials (32-row blocks: binary32 only, C4 single codeword +1 %; the
+      // binary64 32-row blocks measured 1.4 % slower in this form):
       // constant strides from the block base, no bounds, 32-bit offsets (the
       // general form spent ~40 VALU ops of 64-bit address math before the
       // first load); the same loads and sums in the same order

@@ -912,6 +912,32 @@ __device__ __forceinline__ void load_buckets(const uint16_t* __restrict__ il, in
   }
 }
 
+// load_buckets from a workgroup-uniform base and a 32-bit element offset
+// (SGPR base + VGPR offset addressing: no 64-bit address math per load)
+template <int E, int KH>
+__device__ __forceinline__ void load_buckets_off(const uint16_t* __restrict__ base, unsigned off0, int h0, int nhi,
+                                                 int M, int lane, ushort4 (&tb)[KH][(E + 3) / 4]) {
+  constexpr int Q = E < 4 ? E : 4;
+#pragma unroll
+  for (int hh = 0; hh < KH; ++hh) {
+    const int h = h0 + hh < nhi ? h0 + hh : nhi - 1;
+#pragma unroll
+    for (int i = 0; i < E; i += Q) {
+      int e0 = elem_index<E>(lane, i);
+      e0 = e0 < M ? e0 : 0;
+      const unsigned bo = (off0 + (unsigned)(h * M + e0)) * 2u;
+      if constexpr (Q == 4) {
+        tb[hh][i / Q] = ld_off(reinterpret_cast<const ushort4*>(base), bo);
+      } else if constexpr (Q == 2) {
+        const ushort2 t2 = ld_off(reinterpret_cast<const ushort2*>(base), bo);
+        tb[hh][i / Q] = make_ushort4(t2.x, t2.y, 0, 0);
+      } else {
+        tb[hh][i / Q] = make_ushort4(ld_off(base, bo), 0, 0, 0);
+      }
+    }
+  }
+}
+
 template <typename real, int E, int KH>
 __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
                                                const ushort4 (&tb)[KH][(E + 3) / 4], real (&v)[E]) {
@@ -1653,6 +1679,9 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
   real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
   const uint16_t* il = IB ? invs + sidx * a.w + eoff : a.inv + (size_t)lc * a.w + eoff;
+  // the HBM bucket tables as a workgroup-uniform base + this wave's 32-bit offset
+  const uint16_t* ibase = a.inv + (size_t)g * SPW * a.w;
+  const unsigned ioff = (unsigned)((lc - g * SPW) * a.w + eoff);
   const uint32_t* fw = (SPW == 2 ? a.fwd2 : a.fwd3) + (size_t)g * n;
   ushort4 tb[KH][NQ];
   // Ab-table entries of this thread's rows; IB: the ordering values (triples: two words)
@@ -1716,7 +1745,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
         for (int u = 0; u < KR; ++u) { const int r = u * NT + tid; f[u] = fo[r < n ? r : 0]; }
       }
     } else {
-      load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
+      load_buckets_off<EQ, KH>(ibase, ioff, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
     }
     load_section<real, EQ>(bl, bprev, lane, Mq);
     cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
@@ -1778,7 +1807,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   for (int h0 = 0; h0 < a.nhi; h0 += KH) {
     ushort4 tn[KH][NQ];
     const bool more = h0 + KH < a.nhi;
-    if (more) load_buckets<EQ, KH>(il, h0 + KH, a.nhi, M, lane, tn);
+    if (more) {
+      if constexpr (IB) load_buckets<EQ, KH>(il, h0 + KH, a.nhi, M, lane, tn);
+      else load_buckets_off<EQ, KH>(ibase, ioff, h0 + KH, a.nhi, M, lane, tn);
+    }
     gather_buckets<real, EQ, KH>(zs, h0, a.nhi, tb, v);
     if (more) {
 #pragma unroll
@@ -1797,7 +1829,7 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
 #pragma unroll
     for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
       const int r = u * NT + tid;
-      f[u] = fw[r < n ? r : 0];
+      f[u] = ld_off(fw, (unsigned)(r < n ? r : 0) * 4u);  // uniform base + 32-bit offset
     }
   }
   STAMP(3);

@@ -2235,9 +2235,15 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   }
   // the bank-aware step order (build_invb: sign +1 steps first) or h order
   const bool banked = a.invb != nullptr;
+  // binary32: a workgroup-uniform base + this wave's 32-bit offset (SGPR-base
+  // loads; binary64 keeps the per-wave pointer, its scratch grew otherwise)
   const uint16_t* il = (banked ? a.invb : a.inv) + (size_t)lc * a.w;
   ushort4 tb[KH][NQ];
-  load_buckets<E, KH>(il, 0, a.nhi, M, lpos, tb);
+  if constexpr (F64)
+    load_buckets<E, KH>(il, 0, a.nhi, M, lpos, tb);
+  else
+    load_buckets_off<E, KH>((banked ? a.invb : a.inv) + (size_t)g * W * a.w, (unsigned)((lc - g * W) * a.w), 0,
+                            a.nhi, M, lpos, tb);
   // previous beta: all CB codewords up front when registers allow (CB <= 2),
   // else codeword 0 now and codeword c+1 while c is denoised (PB false)
   real bprev[PB ? CB : 2][E];
@@ -2314,7 +2320,13 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     for (int h0 = 0; h0 < a.nhi; h0 += KH) {
       ushort4 tn[KH][NQ];
       const bool more = h0 + KH < a.nhi;
-      if (more) load_buckets<E, KH>(il, h0 + KH, a.nhi, M, lpos, tn);
+      if (more) {
+        if constexpr (F64)
+          load_buckets<E, KH>(il, h0 + KH, a.nhi, M, lpos, tn);
+        else
+          load_buckets_off<E, KH>((banked ? a.invb : a.inv) + (size_t)g * W * a.w, (unsigned)((lc - g * W) * a.w),
+                                  h0 + KH, a.nhi, M, lpos, tn);
+      }
 #pragma unroll
       for (int hh = 0; hh < KH; ++hh) {
         if (h0 + hh < a.nhi) {

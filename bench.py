@@ -64,18 +64,11 @@ def synth_y(op, Pl, sigma, seeds):
 
 
 def sec_bytes(L, M, n, w, B, G, s, kernel="k_sec4"):
-    """Algorithmic bytes of one k_sec launch: the bucket and Ab
-    tables once (uint16 per slot and per section-row; k_sec43 packs a section
-    triple's Ab entries into one uint32 per row), z once per codeword, β read
-    + write, Ab partials written.  k_sec4i / k_sec43i (bucket tables built in
-    LDS from the ordering values) read n ordering values per section instead
-    of the w-entry bucket tables and the Ab table."""
-    if kernel in ("k_sec4i", "k_sec43i"):
-        # bucket tables built in LDS: only the ordering values are read (pairs
-        # one uint32 per row and pair, triples 8 bytes per row and triple)
-        tables = (8 if kernel == "k_sec43i" else 4) * n * G
-    else:
-        tables = 2 * L * w + (4 * n * G if kernel == "k_sec43" else 2 * L * n)
+    """Algorithmic bytes of one section-kernel launch: the bucket
+    and Ab tables once (uint16 per slot and per section-row; k_sec43 packs a
+    section triple's Ab entries into one uint32 per row), z once per codeword,
+    β read + write, Ab partials written."""
+    tables = 2 * L * w + (4 * n * G if kernel == "k_sec43" else 2 * L * n)
     return tables + B * (n * s + 2 * L * M * s + G * n * s)
 
 
@@ -100,17 +93,24 @@ def i8_gemm_ops(L, M, n, B, planes):
 def _cpu_worker(args, barrier, q):
     """One host process: build the oracle operator (untimed), wait at the
     barrier for every other process, then time Tsample AMP iterations of one
-    codeword; puts its (start, end) wall-clock span."""
-    L, M, n, P, sigma, Tsample, seed = args
-    os.environ["OMP_NUM_THREADS"] = "1"
-    from oracle import amp_oracle as orc
-    Ab, Az, _ = orc.sparc_transforms(L, M, n)
-    Pl = P / L * np.ones(L)
-    _, y = orc.rep_inputs(L, M, n, Pl, sigma, Ab, seed)
-    barrier.wait()  # every process starts its timed loop together: no spawn / import stagger in the span
-    t0 = time.time()
-    orc._amp_core(y, Pl, L, M, Tsample, Ab, Az, None, early_stop=False)  # exactly Tsample iterations
-    q.put((t0, time.time()))
+    codeword; puts ("ok", start, end), or ("err", message) on any failure (a
+    failing worker breaks the barrier, so no sibling waits for it)."""
+    try:
+        L, M, n, P, sigma, Tsample, seed = args
+        os.environ["OMP_NUM_THREADS"] = "1"
+        from oracle import amp_oracle as orc
+        Ab, Az, _ = orc.sparc_transforms(L, M, n)
+        Pl = P / L * np.ones(L)
+        _, y = orc.rep_inputs(L, M, n, Pl, sigma, Ab, seed)
+        barrier.wait(timeout=600)  # every process starts its timed loop together
+        t0 = time.time()
+        orc._amp_core(y, Pl, L, M, Tsample, Ab, Az, None, early_stop=False)  # exactly Tsample iterations
+        q.put(("ok", t0, time.time()))
+    except BaseException as e:  # noqa: BLE001 (reported to the parent, never swallowed)
+        try:
+            barrier.abort()
+        finally:
+            q.put(("err", f"{type(e).__name__}: {e}", 0.0))
 
 
 def host_cpus():
@@ -154,13 +154,26 @@ def cpu_baseline(w, procs=None, Tsample=None):
     Tsample = Tsample or T  # a whole decode per process: no extrapolation
     ctx = mp.get_context("spawn")
     barrier, q = ctx.Barrier(procs), ctx.Queue()
-    ps = [ctx.Process(target=_cpu_worker, args=((L, M, n, P, sigma, Tsample, 1000 + i), barrier, q))
+    ps = [ctx.Process(target=_cpu_worker, args=((L, M, n, P, sigma, Tsample, 1000 + i), barrier, q), daemon=True)
           for i in range(procs)]
     for p in ps:
         p.start()
-    spans = [q.get(timeout=600) for _ in ps]
-    for p in ps:
-        p.join(timeout=60)
+    spans, errs = [], []
+    try:
+        for _ in ps:
+            kind, a, b = q.get(timeout=900)
+            if kind == "ok":
+                spans.append((a, b))
+            else:
+                errs.append(a)
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    if errs:
+        raise RuntimeError(f"cpu_baseline: {len(errs)} of {procs} workers failed: {errs[0]}")
     wall = max(e for _, e in spans) - min(s for s, _ in spans)
     per_core = float(np.mean([e - s for s, e in spans])) / Tsample
     return {
@@ -231,27 +244,35 @@ def valu_bound(tag, kernel, kernel_ms, cus, clock_ghz=2.4):
             "source": src, "clock_ghz_assumed": clock_ghz}
 
 
-PROFILE_TAGS = {  # (workload, codewords, backend) -> scripts/profile_r*.sh tag (binary32)
-    ("c2", 1, "hadamard"): "c2", ("c4", 1, "hadamard"): "c4b1", ("c3", 256, "hadamard"): "c3",
-    ("c4", 256, "hadamard"): "c4", ("c3", 256, "dense"): "c3dense", ("c4", 1, "dense"): "dense_l768",
+PROFILE_TAGS = {  # (workload, codewords, backend, precision) -> scripts/profile_r04.sh tag
+    ("c2", 1, "hadamard", "fp32"): "c2", ("c4", 1, "hadamard", "fp32"): "c4b1",
+    ("c3", 256, "hadamard", "fp32"): "c3", ("c4", 256, "hadamard", "fp32"): "c4",
+    ("c3", 256, "dense", "fp32"): "c3dense", ("c4", 1, "dense", "fp32"): "dense_l768",
+    ("c2", 1, "hadamard", "fp64"): "c2f64", ("c3", 256, "hadamard", "fp64"): "c3f64",
 }
 
 
-def load_graph_median(tag, kernel):
-    """In-graph launch duration of `kernel` (ns): the median over the
-    graph-replayed decodes of the newest committed
-    profiles/<round>_<tag>_graph_trace.txt (rocprofv3 kernel trace of the same
-    bench command, scripts/graph_trace.py), with that file's name; or None."""
+def load_trace(tag, kernel):
+    """The graph-replay durations of `kernel` from the newest committed
+    profiles/<round>_<tag>_graph_trace.txt (scripts/graph_trace.py): median
+    in-graph duration and exclusive duration (ns), launch count, the sources
+    hash the profile was taken of, and the file; or None."""
     import glob
     import re
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{tag}_graph_trace.txt")))
     if not files:
         return None
+    src, hit = None, None
     for line in open(files[-1]):
-        m = re.match(r"(\S+)\s+n=\s*(\d+)\s+duration median\s+(\d+) ns", line)
+        if line.startswith("sources sha256 "):
+            src = line.split()[-1]
+        m = re.match(r"(\S+)\s+n=\s*(\d+)\s+duration median\s+(\d+) ns.*?(?:exclusive median\s+(\d+) ns)?", line)
         if m and m.group(1) == kernel:
-            return float(m.group(3)), int(m.group(2)), os.path.relpath(files[-1], ROOT)
-    return None
+            hit = (float(m.group(3)), float(m.group(4)) if m.group(4) else None, int(m.group(2)))
+    if hit is None:
+        return None
+    return {"duration_ns": hit[0], "exclusive_ns": hit[1], "launches": hit[2], "sources": src,
+            "file": os.path.relpath(files[-1], ROOT)}
 
 
 def load_pmc(workload, kernel):
@@ -262,6 +283,104 @@ def load_pmc(workload, kernel):
         return d.get(workload, {}).get(kernel)
     except (OSError, ValueError):
         return None
+
+
+def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
+    """Roofline of the dominant kernel of one decode of B codewords.
+
+    `achieved` = algorithmic bytes (ops) per launch / the kernel's mean launch
+    duration measured LIVE here with HIP events on the library's stream: each
+    launch of a short eager decode issued PROFILE_REP times back to back
+    between one event pair (kernel + same-stream boundary, the quantity that
+    adds up to a decode).  Beside it: the committed rocprofv3 graph trace of
+    the same command (`trace`: its exclusive in-graph duration and whether it
+    was taken of these sources), PMC HBM traffic (only when taken of these
+    sources), and a consistency check T x (sum of per-iteration kernel times)
+    <= ms_per_step."""
+    from sparc_ldpc_amd._lib import source_hash
+    kinds, total_ms = op.profile(B, T, early_stop=False)
+    kinds_rep, _ = op.profile(B, min(T, 4), early_stop=False, rep=PROFILE_REP)
+    s = 8 if precision == "fp64" else 4
+    plan = op.plan(B)
+    mfma = plan["section_kernel"] == "dense_mfma"
+    if op.backend == "hadamard":
+        G = plan["partials"]
+        per = {"k_sec": sec_bytes(L, M, n, op.w, B, G, s, plan["section_kernel"]), "k_row": row_bytes(n, B, G, s)}
+    elif mfma:
+        per = {"k_dense_az": i8_gemm_ops(L, M, n, B, NP_Z), "k_dense_ab": i8_gemm_ops(L, M, n, B, NP_B)}
+    else:
+        per = {"k_dense_az": gemv_bytes(L, M, n) * B, "k_dense_ab": gemv_bytes(L, M, n) * B,
+               "k_dense_den": B * (8 * 4 * L * M + 8 * L * M), "k_row": row_bytes(n, B, 8, s)}
+    share = {k: kinds[k][0] * kinds[k][1] for k in per}
+    dom = max(share, key=share.get)
+    dom_ms = kinds_rep[dom][0]
+    scale = 1e12 if mfma else 1e9
+    peak = I8_PEAK_TOPS if mfma else HBM_PEAK_GBS
+    achieved = per[dom] / (dom_ms * 1e-3) / scale
+    kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom)
+    trace_name = {"k_dense_az": "k_gemm_i8_Az", "k_dense_ab": "k_gemm_i8_Ab"}[dom] if mfma else kname
+    if mfma:
+        kname = "k_gemm_i8 (" + {"k_dense_az": f"A^T z, {NP_Z} digit planes",
+                                 "k_dense_ab": f"A beta, {NP_B} digit planes"}[dom] + ")"
+    src = source_hash()
+    # consistency: the loop kernels' back-to-back times per iteration, T times
+    per_iter = sum(kinds_rep[k][0] * round(kinds[k][1] / T) for k in kinds if kinds[k][1] >= T)
+    roof = {
+        "bound": "mfma" if mfma else "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": peak,
+        "unit": "TFLOP/s" if mfma else "GB/s", "frac": round(achieved / peak, 4), "traffic": None,
+        ("algorithmic_int8_ops_per_launch" if mfma else "algorithmic_bytes_per_launch"): per[dom],
+        **({"ops": "int8 multiply-adds x 2 (TOP/s)"} if mfma else {}),
+        "avg_launch_ms": round(dom_ms, 5),
+        "timing": f"HIP events on the library stream around {PROFILE_REP} back-to-back launches of each kernel "
+                  f"(kernel + same-stream boundary), measured live in this run",
+        "kernel_ms": {k: round(v[0], 5) for k, v in kinds_rep.items() if v[1]},
+        "kernel_ms_event_bracketed": {k: round(v[0], 5) for k, v in kinds.items() if v[1]},
+        "eager_decode_ms": round(total_ms, 3),
+        "consistency": {"per_iteration_ms": round(per_iter, 5), "T": T, "T_x_per_iteration_ms": round(T * per_iter, 4),
+                        "ms_per_step": ms_per_step, "ok": bool(T * per_iter <= ms_per_step * 1.02)},
+        "sources": src,
+    }
+    tag = PROFILE_TAGS.get((args.workload, B, op.backend, precision))
+    tr = load_trace(tag, trace_name) if tag else None
+    if tr is not None:
+        match = tr["sources"] == src
+        t = {"file": tr["file"], "profile_matches_build": match, "launches": tr["launches"],
+             "in_graph_duration_ms": round(tr["duration_ns"] * 1e-6, 5)}
+        if tr["exclusive_ns"]:
+            ex_ms = tr["exclusive_ns"] * 1e-6
+            t["exclusive_ms"] = round(ex_ms, 5)
+            t["frac_exclusive"] = round(per[dom] / (ex_ms * 1e-3) / scale / peak, 4)
+        roof["trace"] = t
+    pmc = load_pmc(f"{args.workload}_{op.backend}_{precision}_B{B}", trace_name)
+    if pmc is not None:
+        if pmc.get("sources") == src:
+            roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+            roof["traffic_over_algorithmic"] = round(pmc["hbm_bytes_per_launch"] / per[dom], 3) if not mfma else None
+        else:
+            roof["traffic_stale"] = {"hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch"),
+                                     "sources": pmc.get("sources"), "note": "PMC pass of other sources: not used"}
+    if kname == "k_secb" and precision == "fp32":
+        vb = valu_bound(args.workload, kname, dom_ms, plan["cus"])
+        if vb is not None:
+            roof["secondary_bound"] = dict(bound="latency", **vb)
+    return roof
+
+
+def timed_steps(op, B, T, steps, warmup):
+    """Warmup, then exactly `steps` decodes between barrier + device sync on
+    both sides; returns (this rank's seconds, the max over ranks)."""
+    from sparc_ldpc_amd import dist
+    for _ in range(warmup):
+        op.run(B, T, early_stop=False)
+    op.wait()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        op.run(B, T, early_stop=False)
+    op.wait()
+    dist.barrier()
+    mine = time.perf_counter() - t0
+    return mine, float(dist.allreduce_max(np.array([mine]))[0])
 
 
 def main():
@@ -312,94 +431,11 @@ def main():
     op.reserve(B, T)
     op.stage(y, Pl)
 
-    def sync_all():
-        op.wait()
-        dist.barrier()
-
-    for _ in range(args.warmup):
-        op.run(B, T, early_stop=False)
-    sync_all()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        op.run(B, T, early_stop=False)
-    sync_all()
-    elapsed = time.perf_counter() - t0
-    elapsed = float(dist.allreduce_max(np.array([elapsed]))[0])  # the slowest rank's time
-
-    # per-kernel device times over one eager decode (HIP events on the
-    # library's stream), for the roofline of the dominant kernel
-    kinds, total_ms = op.profile(B, T, early_stop=False)
-    # the roofline's launch duration: each launch of a short eager decode
-    # issued REP times back to back between two HIP events on the library's
-    # stream (mean = elapsed / REP: kernel + same-stream boundary, without the
-    # event packets' own dispatch overhead that a per-launch bracket adds)
-    kinds_rep, _ = op.profile(B, min(T, 4), early_stop=False, rep=PROFILE_REP)
-    s = 8 if args.precision == "fp64" else 4
-    plan = op.plan(B)
-    if args.backend == "hadamard":
-        G = plan["partials"]  # Ab partials per codeword of the section kernel this batch runs
-        wv = op.w
-        sk = plan["section_kernel"]
-        per = {
-            "k_sec": sec_bytes(L, M, n, wv, B, G, s, sk.rstrip("f")),
-            "k_row": row_bytes(n, B, G, s),
-        }
-        if sk.endswith("f"):  # the fused kernel also does the row step (k_row: the last one only)
-            per["k_sec"] += per["k_row"]
-    elif plan["section_kernel"] == "dense_mfma":
-        per = {"k_dense_az": i8_gemm_ops(L, M, n, B, NP_Z), "k_dense_ab": i8_gemm_ops(L, M, n, B, NP_B)}
-    else:
-        per = {"k_dense_az": gemv_bytes(L, M, n) * B, "k_dense_ab": gemv_bytes(L, M, n) * B,
-               "k_dense_den": B * (8 * 4 * L * M + 8 * L * M), "k_row": row_bytes(n, B, 8, s)}
-    share = {k: kinds[k][0] * kinds[k][1] for k in per}
-    dom = max(share, key=share.get)
-    dom_ms = kinds_rep[dom][0]
-    mfma = plan["section_kernel"] == "dense_mfma"
-    achieved = per[dom] / (dom_ms * 1e-3) / (1e12 if mfma else 1e9)
-    peak = I8_PEAK_TOPS if mfma else HBM_PEAK_GBS
-    kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom)
-    # the kernel's name in the rocprofv3 traces (k_gemm_i8 is one template, two products)
-    trace_name = {"k_dense_az": "k_gemm_i8_Az", "k_dense_ab": "k_gemm_i8_Ab"}[dom] if mfma else kname
-    pmc = load_pmc(f"{args.workload}_{args.backend}_{args.precision}_B{B}", trace_name)
-    if mfma:
-        kname = "k_gemm_i8 (" + {"k_dense_az": f"A^T z, {NP_Z} digit planes",
-                                 "k_dense_ab": f"A beta, {NP_B} digit planes"}[dom] + ")"
-    scale = 1e12 if mfma else 1e9
-    # headline: the launch duration INSIDE the replayed decode graph (the
-    # rocprofv3 graph-trace median of this same bench command, committed under
-    # profiles/), where the kernel follows the row kernel's writes on other
-    # XCDs; beside it the live HIP-event figure of REP back-to-back launches
-    # (inputs still in the caches from the previous launch: a few % faster)
-    tag = PROFILE_TAGS.get((args.workload, B, args.backend)) if args.precision == "fp32" else None
-    gm = load_graph_median(tag, trace_name) if tag else None
-    ev = {"achieved": round(achieved, 1), "frac": round(achieved / peak, 4), "avg_launch_ms": round(dom_ms, 5),
-          "timing": f"HIP events on the library stream around {PROFILE_REP} back-to-back launches per kernel, "
-                    f"measured live in this run"}
-    if gm is not None:
-        g_ms = gm[0] * 1e-6
-        ach_g = per[dom] / (g_ms * 1e-3) / scale
-        head = {"achieved": round(ach_g, 1), "frac": round(ach_g / peak, 4), "avg_launch_ms": round(g_ms, 5),
-                "timing": f"in-graph launch duration: median of {gm[1]} graph-replayed launches, rocprofv3 "
-                          f"kernel trace of this bench command ({gm[2]})"}
-    else:
-        head = ev
-    roofline = {
-        "bound": "mfma" if mfma else "hbm", "kernel": kname, "achieved": head["achieved"], "peak": peak,
-        "unit": "TFLOP/s" if mfma else "GB/s", "frac": head["frac"],
-        "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-        ("algorithmic_int8_ops_per_launch" if mfma else "algorithmic_bytes_per_launch"): per[dom],
-        **({"ops": "int8 multiply-adds x 2 (TOP/s)"} if mfma else {}),
-        "avg_launch_ms": head["avg_launch_ms"], "timing": head["timing"],
-        **({"events": ev} if gm is not None else {}),
-        "kernel_ms": {k: round(v[0], 5) for k, v in kinds_rep.items() if v[1]},
-        "kernel_ms_event_bracketed": {k: round(v[0], 5) for k, v in kinds.items() if v[1]},
-        "eager_decode_ms": round(total_ms, 3),
-    }
-
-    if kname == "k_secb" and args.precision == "fp32":
-        vb = valu_bound(args.workload, kname, head["avg_launch_ms"], plan["cus"])
-        if vb is not None:
-            roofline["secondary_bound"] = dict(bound="latency", **vb)
+    mine, elapsed = timed_steps(op, B, T, args.steps, args.warmup)
+    # every rank's own rate (weak scaling: the spread shows a slow GPU)
+    times = dist.allreduce_sum(np.eye(world)[rank] * mine) if world > 1 else np.array([mine])
+    ms_per_step = round(elapsed / args.steps * 1e3, 4)
+    roofline = measure_roofline(op, args, L, M, n, B, T, args.precision, ms_per_step)
     result = {
         "metric": f"decoded codewords/sec (T AMP iters) at L={L},M={M}; achieved HBM GB/s vs roofline",
         "value": round(B * args.steps * world / elapsed, 3),
@@ -407,7 +443,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -418,33 +454,33 @@ def main():
                    "early_stop": False, "parallelism": f"reps sharded over {world} GPU(s)"},
         "roofline": roofline,
     }
+    if world > 1:
+        rates = B * args.steps / np.asarray(times)
+        result["per_rank"] = {"value_min": round(float(rates.min()), 3), "value_max": round(float(rates.max()), 3),
+                              "ms_per_step": [round(float(t) / args.steps * 1e3, 4) for t in times]}
     if args.precision == "fp32" and args.backend == "hadamard" and not args.no_fp64:
         # the same workload in binary64 (the reference's precision; the joint
-        # decoder's): same seeds, same timing protocol, every rank
+        # decoder's): same seeds, same timing protocol, every rank, with its
+        # own live roofline
         op64 = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="hadamard", precision="fp64",
                                 device=device)
         op64.reserve(B, T)
         op64.stage(y, Pl)
-        for _ in range(args.warmup):
-            op64.run(B, T, early_stop=False)
-        op64.wait()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            op64.run(B, T, early_stop=False)
-        op64.wait()
-        dist.barrier()
-        e64 = float(dist.allreduce_max(np.array([time.perf_counter() - t0]))[0])
+        _, e64 = timed_steps(op64, B, T, args.steps, args.warmup)
+        ms64 = round(e64 / args.steps * 1e3, 4)
         result["fp64_leg"] = {"value": round(B * args.steps * world / e64, 3), "unit": "codewords/s",
-                              "ms_per_step": round(e64 / args.steps * 1e3, 4), "dtype": "f64",
-                              "section_kernel": op64.plan(B)["section_kernel"]}
+                              "ms_per_step": ms64, "dtype": "f64",
+                              "section_kernel": op64.plan(B)["section_kernel"],
+                              "roofline": measure_roofline(op64, args, L, M, n, B, T, "fp64", ms64)}
         del op64
     if rank == 0 and world == 1 and not args.no_dense:
         try:
             result["dense_gemv"] = dense_gemv_probe(device)
         except Exception as e:  # report, never hide
             result["dense_gemv"] = {"error": str(e)}
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
+        # after the timed region (every rank), on rank 0's host cores: the
+        # N-rank line carries its own CPU baseline
         result["cpu_baseline"] = cpu_baseline(w, args.cpu_procs or None)
         result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
     if rank == 0:

@@ -42,9 +42,12 @@ enum {
   SA_BACKEND_DENSE = 1,     /* materialised n x (L*M) design matrix: fp32 GEMVs for B < 4
                                codewords, int8 matrix-core GEMMs on exact +-1 entries with
                                three-digit fixed-point vectors for B >= 4 */
-  SA_BACKEND_HOST = 2       /* no device operator: the caller's own Ab / Az (any operator, as the
+  SA_BACKEND_HOST = 2,      /* no device operator: the caller's own Ab / Az (any operator, as the
                                reference's amp() accepts any callables) applied on the host, the
                                loop's tau, denoiser and residual on the device (sa_host_*) */
+  SA_BACKEND_MATRIX = 3     /* a caller's own dense n x (L*M) design matrix (e.g. i.i.d. Gaussian;
+                               sa_create_matrix) held on the device in the context precision:
+                               GEMVs for B < 4 codewords, f32 / f64 MFMA GEMMs for B >= 4 */
 };
 
 enum { SA_PREC_F32 = 0, SA_PREC_F64 = 1 };
@@ -64,6 +67,42 @@ enum {
  * the reference's RandomState algorithm (sparc_ldpc.py:107-117). */
 int sa_create(sa_ctx** out, int L, int M, int n, const uint32_t* ordering,
               int backend, int precision, int device);
+
+/* sa_create with plan options: which kernels and layouts a decode uses is
+ * normally chosen by built-in rules from (L, M, n, precision, batch, CUs)
+ * (sa_plan reports the choice); these bits override a rule, e.g. to test a
+ * kernel on shapes where the rule would not pick it.  Every option keeps the
+ * results within the same parity bounds; SA_PLAN_NO_PT and SA_PLAN_EAGER are
+ * bit-identical to the default plan.  `sa_subset` contexts
+ * inherit their parent's options. */
+enum {
+  SA_PLAN_DEFAULT = 0,
+  SA_PLAN_SEC3 = 1 << 0,      /* one codeword: three sections per workgroup (k_sec43) where it fits */
+  SA_PLAN_NO_SEC3 = 1 << 1,   /* one codeword: never k_sec43 (pairs, k_sec4) */
+  SA_PLAN_ROW16 = 1 << 2,     /* one codeword: 16-row k_row2 blocks where they fit */
+  SA_PLAN_NO_ROW16 = 1 << 3,  /* one codeword: 32-row k_row2 blocks */
+  SA_PLAN_NO_PT = 1 << 4,     /* Ab partials [G][n] instead of row-block major (bit-identical) */
+  SA_PLAN_ZIL = 1 << 5,       /* batched: z / Ab partials codeword-interleaved (binary64 too) */
+  SA_PLAN_NO_ZIL = 1 << 6,    /* batched: z / Ab partials [B][n] (binary32 too) */
+  SA_PLAN_WB8 = 1 << 7,       /* batched: 8 sections per workgroup */
+  SA_PLAN_WB16 = 1 << 8,      /* batched: 16 sections per workgroup */
+  SA_PLAN_NO_BANKS = 1 << 9,  /* batched: bucket slots summed in h order (no bank-aware slot order) */
+  SA_PLAN_EAGER = 1 << 10,    /* sa_run launches eagerly instead of replaying a captured hipGraph */
+  SA_PLAN_ALL = (1 << 11) - 1
+};
+int sa_create_ex(sa_ctx** out, int L, int M, int n, const uint32_t* ordering,
+                 int backend, int precision, int device, int plan);
+
+/* A caller's own dense design (the reference's amp() with any pair of
+ * callables, sparc_ldpc.py:189,213,220, e.g. Ab = lambda b: A @ b,
+ * Az = lambda z: A.T @ z for an i.i.d. Gaussian A): A is n x (L*M) row-major
+ * binary64, copied to the device in `precision`; the context's sa_Ab / sa_Az
+ * compute A beta / A^T z (no 1/sqrt(n): the matrix is used as given) and
+ * sa_amp / sa_run run the whole loop on the device.  Section sizes M need not
+ * be powers of two.  sa_encode / sa_cancel / sa_subset need an ordering
+ * (SA_ERR_UNSUPPORTED here). */
+int sa_create_matrix(sa_ctx** out, int L, int M, int n, const double* A,
+                     int precision, int device);
 
 /* Replaces sparc_transforms_shorter(L, M, n, ordering[sections])
  * (ldpc/sparc_ldpc.py:154-168; called with a fancy-indexed subset at
@@ -214,10 +253,10 @@ int sa_host_residual(sa_ctx* ctx, int B, int t, int flags, const double* ab);
 /* Introspection. */
 /* The kernels a decode of B codewords runs: out8 = {section kernel (0 k_sec,
  * 1 k_sec2, 2 k_secb, 3 dense fp32 GEMVs, 4 k_sec4, 5 k_sec43, 6 dense int8
- * MFMA GEMMs, 7 k_sec4f / 8 k_sec43f: the row step fused into the section
- * kernel), Ab partials per codeword, row splits,
+ * MFMA GEMMs, 7 caller-matrix f32 / f64 MFMA GEMMs), Ab partials per codeword, row splits,
  * codewords per batched workgroup, z^2 partials, w, row kernel (1 k_row2,
- * 2 k_rowv 16-byte rows, 3 k_rowv 8-byte rows, 0 k_row), number of CUs}. */
+ * 2 k_rowv 16-byte rows, 3 k_rowv 8-byte rows, 0 k_row, 4 k_row2 16-row
+ * blocks, 5 k_rowc), number of CUs}. */
 int sa_plan(sa_ctx* ctx, int B, int64_t* out8);
 int sa_info(const sa_ctx* ctx, int64_t* out8); /* L, M, n, w, backend, precision, device, bytes */
 int sa_device_count(void);

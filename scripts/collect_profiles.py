@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy the round's profile summaries from gpurun_out/ (scripts/profile_r02.sh)
+"""Copy the round's profile summaries from gpurun_out/ (scripts/profile_r04.sh)
 into profiles/<round>_*: kernel stats, PMC traffic per launch (also merged
 into profiles/pmc_traffic.json under the bench's workload key), the
 graph-replayed kernel durations, SQ counters and phase stamps."""
@@ -9,7 +9,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RND = sys.argv[1] if len(sys.argv) > 1 else "r03"
+RND = sys.argv[1] if len(sys.argv) > 1 else "r04"
 # tag -> bench.py load_pmc key (workload_backend_precision_B)
 KEYS = {"c2": "c2_hadamard_fp32_B1", "c4b1": "c4_hadamard_fp32_B1", "c3": "c3_hadamard_fp32_B256",
         "c4": "c4_hadamard_fp32_B256",
@@ -30,9 +30,12 @@ def main():
             for f in fs:
                 if f.endswith("kernel_trace.csv"):
                     tr = os.path.join(dp, f)
+        bt = os.path.join(out, f"prof_{tag}", "build.txt")
+        src = open(bt).read().strip() if os.path.exists(bt) else "unknown"
         if tr:
             subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "graph_trace.py"), tr,
-                            os.path.join(dst, f"{RND}_{tag}_graph_trace.txt")], check=False, stdout=subprocess.DEVNULL)
+                            os.path.join(dst, f"{RND}_{tag}_graph_trace.txt"), src], check=False,
+                           stdout=subprocess.DEVNULL)
     for tag in ("c2", "c3", "c3dense"):
         p = os.path.join(out, f"sq_{tag}.txt")
         if os.path.exists(p):

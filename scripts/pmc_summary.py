@@ -25,7 +25,7 @@ def short(name):
         return "k_gemm_i8_Az"   # three digit planes of z
     if "k_gemm_i8<4>" in name:
         return "k_gemm_i8_Ab"   # four digit planes of beta
-    for k in ("k_secb", "k_sec2", "k_sec43f", "k_sec43", "k_sec4f", "k_sec4", "k_sec8", "k_sec", "k_row2", "k_rowv", "k_rowc", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide",
+    for k in ("k_secb", "k_sec2", "k_sec43", "k_sec4", "k_sec8", "k_sec", "k_row2", "k_rowv", "k_rowc", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide",
               "k_gemm_i8", "k_i8_quant", "k_i8_build",
               "k_bp", "k_llr", "k_bp2sp", "k_sp_norm", "k_colsum"):
         if any(p in name for p in (f"::{k}<", f" {k}<", f" {k}(", f"::{k}(")) or name.startswith((f"{k}<", f"{k}(")):
@@ -55,11 +55,13 @@ def main():
     fetch = counters(os.path.join(out, "fetch"), "FETCH_SIZE")
     write = counters(os.path.join(out, "write"), "WRITE_SIZE")
     res = {}
+    bt = os.path.join(out, "build.txt")
+    src = open(bt).read().strip() if os.path.exists(bt) else None
     for k in sorted(set(fetch) | set(write)):
         fk, wk = fetch.get(k, 0.0), write.get(k, 0.0)
         res[k] = {"fetch_kib_raw": fk, "write_kib": wk,
                   "hbm_bytes_per_launch": int((2 * fk + wk) * 1024),
-                  "hbm_bytes_per_launch_raw": int((fk + wk) * 1024)}
+                  "hbm_bytes_per_launch_raw": int((fk + wk) * 1024), "sources": src, "round": rnd}
     with open(os.path.join(dst, f"{rnd}_{tag}_pmc.json"), "w") as fh:
         json.dump(res, fh, indent=1)
     p = os.path.join(dst, "pmc_traffic.json")

@@ -10,6 +10,8 @@ export TMPDIR=/tmp
 TAG=${1:-run}; shift
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+# the identity of the build being profiled (bench.py compares it with its own)
+python3 -c "from sparc_ldpc_amd._lib import source_hash; print(source_hash())" > $OUT/build.txt || exit 1
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- \

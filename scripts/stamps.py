@@ -23,17 +23,9 @@ lib = sp.load_library()
 lib.sa_debug_stamps.argtypes = [ct.POINTER(ct.c_ulonglong)]
 # stamp order in time (index 10: after an explicit wait for every global load
 # issued so far, i.e. the bucket-table / previous-beta / Ab-table loads)
-if op.plan(B)["section_kernel"] in ("k_sec4f", "k_sec43f"):  # the fused kernels (SPARC_AMP_FUSE=1)
-    order = [0, 11, 12, 1, 2, 10, 3, 4, 5, 6, 7, 8, 9]
-    names = ["row step", "arrive+wait", "z+tau", "z->LDS+bar", "wait tables", "gather", "fwht1", "denoise",
-             "fwht2", "ts+bar", "rows", "drain"]
-elif op.plan(B)["section_kernel"] == "k_secb":
+if op.plan(B)["section_kernel"] == "k_secb":
     order = [0, 1, 2, 3, 4, 5, 6, 7]
     names = ["loads+tau", "z->LDS+bar", "gather", "fwht+denoise+fwht", "T->LDS+bar", "rows", "drain"]
-elif op.plan(B)["section_kernel"] in ("k_sec4i", "k_sec43i"):  # bucket tables built in LDS (SPARC_AMP_IB=1)
-    order = [0, 1, 2, 10, 13, 3, 4, 5, 6, 7, 8, 9]
-    names = ["tau+loads", "z->LDS+bar", "wait loads", "scatter+bar", "gather", "fwht1", "denoise", "fwht2",
-             "ts+bar", "rows", "drain"]
 else:
     order = [0, 1, 2, 10, 3, 4, 5, 6, 7, 8, 9]
     names = ["tau+loads", "z->LDS+bar", "wait tables", "gather", "fwht1", "denoise", "fwht2", "ts+bar", "rows",

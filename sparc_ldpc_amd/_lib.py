@@ -27,15 +27,40 @@ SA_ERR_NO_DEVICE = -6
 SA_BACKEND_HADAMARD = 0
 SA_BACKEND_DENSE = 1
 SA_BACKEND_HOST = 2
+SA_BACKEND_MATRIX = 3
 SA_PREC_F32 = 0
 SA_PREC_F64 = 1
 SA_FLAG_NO_EARLY_STOP = 1
 SA_FLAG_BETA0 = 0x100
 SA_PTR_DEVICE = 0x200
 
+# sa_create_ex plan options (include/sparc_amp.h): overrides of the built-in
+# kernel / layout choice rules, by name
+SA_PLAN = {
+    "SEC3": 1 << 0, "NO_SEC3": 1 << 1, "ROW16": 1 << 2, "NO_ROW16": 1 << 3, "NO_PT": 1 << 4,
+    "ZIL": 1 << 5, "NO_ZIL": 1 << 6, "WB8": 1 << 7, "WB16": 1 << 8, "NO_BANKS": 1 << 9, "EAGER": 1 << 10,
+}
+
+
+def plan_bits(plan) -> int:
+    """None / an int / an iterable of SA_PLAN names -> the option bits."""
+    if plan is None:
+        return 0
+    if isinstance(plan, int):
+        return plan
+    if isinstance(plan, str):
+        plan = [plan]
+    bits = 0
+    for name in plan:
+        key = name.upper()
+        if key not in SA_PLAN:
+            raise ValueError(f"unknown plan option {name!r}; known: {sorted(SA_PLAN)}")
+        bits |= SA_PLAN[key]
+    return bits
+
 # Every symbol include/sparc_amp.h declares (tests check the export table).
 EXPORTS = (
-    "sa_create", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
+    "sa_create", "sa_create_ex", "sa_create_matrix", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
     "sa_reserve", "sa_stage", "sa_stage_power_batch", "sa_run", "sa_wait", "sa_fetch", "sa_fetch_z", "sa_run_event_ms",
     "sa_profile", "sa_profile_rep", "sa_profile_kinds", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
@@ -48,6 +73,8 @@ _I = ct.c_int
 _D = ct.POINTER(ct.c_double)
 _SIG = {
     "sa_create": (_I, [ct.POINTER(_P), _I, _I, _I, ct.POINTER(ct.c_uint32), _I, _I, _I]),
+    "sa_create_ex": (_I, [ct.POINTER(_P), _I, _I, _I, ct.POINTER(ct.c_uint32), _I, _I, _I, _I]),
+    "sa_create_matrix": (_I, [ct.POINTER(_P), _I, _I, _I, _D, _I, _I]),
     "sa_subset": (_I, [_P, ct.POINTER(ct.c_int64), _I, ct.POINTER(_P)]),
     "sa_destroy": (None, [_P]),
     "sa_Ab": (_I, [_P, _I, _D, _D]),
@@ -87,6 +114,27 @@ _SIG = {
 
 _lib = None
 
+_SRC_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+_INC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+
+
+def source_hash() -> str:
+    """SHA-256 (first 16 hex digits) over the HIP sources and C headers the
+    libraries are built from (csrc/*.hip, csrc/Makefile, include/*.h, in name
+    order): the identity a committed profile records and bench.py compares
+    against, so a roofline figure is only read from a profile of this build."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(_SRC_DIR) if f.endswith(".hip") or f == "Makefile")
+    paths = [os.path.join(_SRC_DIR, f) for f in files]
+    if os.path.isdir(_INC_DIR):
+        paths += [os.path.join(_INC_DIR, f) for f in sorted(os.listdir(_INC_DIR)) if f.endswith(".h")]
+    for p in paths:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
 
 class SparcAmpError(RuntimeError):
     """A non-zero status from libsparc_amp.so."""
@@ -107,6 +155,11 @@ def load(path: str = LIB_PATH) -> ct.CDLL:
             "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = ct.CDLL(path)
     for name, (res, args) in _SIG.items():
+        # an older build (A/B runs against a previous library) may lack newer
+        # entry points: they stay untyped and absent; the export test pins the
+        # current build to the full list
+        if not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -63,11 +63,6 @@ int fail(int code, const std::string& msg) {
 
 using f4 = float __attribute__((ext_vector_type(4)));
 
-// Streaming (non-temporal) 16-B load of the design matrix: read once per pass.
-__device__ __forceinline__ float4 ld_stream(const float* p) {
-  const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
 
 
 // Load of a uniform value as a VECTOR load (opaque zero lane offset): a scalar
@@ -759,10 +754,6 @@ struct SecArgs {
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
   const uint32_t* __restrict__ fwd3; // [ceil(L/3)][n] a section triple, 10-bit fields k | sign<<9 (M <= 512)
-  // the ordering values themselves (bucket tables built in LDS, SecArgs::ib):
-  // [ceil(L/2)][n] o_0 | o_1 << 16 (pairs), [ceil(L/3)][n] (o_0 | o_1 << 16, o_2) (triples)
-  const uint32_t* __restrict__ fwo2;
-  const uint2* __restrict__ fwo3;
   const real* __restrict__ c;        // [L] sqrt(n * Pl), or [B][L] per codeword (cst = L)
   const real* __restrict__ z;        // [B][n]
   real* __restrict__ beta;           // [B][L*M] previous estimate (read)
@@ -791,7 +782,7 @@ template <typename real>
 struct RowArgs {
   const real* __restrict__ y;    // [B][n]
   real* __restrict__ z;          // [B][n] the residual (k_row2: the new one is written here)
-  const real* __restrict__ z_in; // [B][n] k_row2: the previous residual (= z unless the fused path double-buffers it)
+  const real* __restrict__ z_in; // [B][n] the previous residual (= z)
   const real* __restrict__ abp;  // [B][G][n]
   const real* __restrict__ bbp;  // [B][G]
   real* __restrict__ zzp;        // [B][NZ]
@@ -858,12 +849,8 @@ struct ZStage {
 // issued at once; the barrier that follows waits for it (vmcnt).  Returns
 // false (nothing issued) when z is not 16-B aligned: ZStage then.  c2: k_sec4
 // 7.51 -> 7.26 us, +2 % codewords/s.
-constexpr int kAuxSc1 = 16;  // cache-policy operand of global_load_lds: sc1 (checked in the ISA)
 template <typename real, int NT, int AUX = 0>
 __device__ __forceinline__ bool stage_z_dma(const real* zb, real* zs, int n, int tid) {
-#ifdef SA_NO_DMA
-  return false;
-#endif
   if (reinterpret_cast<uintptr_t>(zb) & 15) return false;
   const int lane = tid & 63, nbytes = n * (int)sizeof(real);
   for (int ch = tid >> 6; ch * 1024 < nbytes; ch += NT / 64) {
@@ -880,11 +867,10 @@ __device__ __forceinline__ bool stage_z_dma(const real* zb, real* zs, int n, int
 
 // After stage_z_dma: the < 16-B tail of z by ordinary loads, and the zero
 // slot zs[n] (gathered for empty buckets).
-template <typename real, bool SC1 = false>
+template <typename real>
 __device__ __forceinline__ void finish_z_dma(const real* zb, real* zs, int n, int tid) {
   const int n0 = n * (int)sizeof(real) / 16 * 16 / (int)sizeof(real);
-  if (tid < n - n0)
-    zs[n0 + tid] = SC1 ? __hip_atomic_load(zb + n0 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : zb[n0 + tid];
+  if (tid < n - n0) zs[n0 + tid] = zb[n0 + tid];
   if (tid == 0) zs[n] = 0;
 }
 
@@ -956,11 +942,7 @@ __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
           const unsigned short rr[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
-#ifdef SA_DIAG_GATHER_FAKE  // diagnostic (stamps builds): conflict-free consecutive rows, wrong results
-            zz[hh][i + q] = zs[((threadIdx.x & 63) * Q + q + (rr[q] & 1)) & 4095];
-#else
             zz[hh][i + q] = zs[rr[q]];
-#endif
           }
         }
       if constexpr (KH * E > 16) {
@@ -1008,11 +990,7 @@ __device__ __forceinline__ void gather_buckets(const real* zs, int h0, int nhi,
         const unsigned short rr[4] = {r4.x, r4.y, r4.z, r4.w};
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-#ifdef SA_DIAG_GATHER_FAKE  // diagnostic (stamps builds): conflict-free consecutive rows, wrong results
-          const real zz = zs[((threadIdx.x & 63) * Q + q + (rr[q] & 1)) & 4095];
-#else
           const real zz = zs[rr[q]];
-#endif
           v[i + q] += neg ? -zz : zz;
         }
       }
@@ -1485,173 +1463,17 @@ __device__ __forceinline__ real combine_q(const real* red, int w0, int f) {
   return x[0];
 }
 
-// ---- fused row step: k_row2 of iteration t-1 at the head of the section
-// kernel of iteration t (one codeword; the section workgroups all resident)
-//
-// Two kernels per iteration pay two dependent kernel boundaries.  The fused
-// kernel K_t does the row step of t-1 first (each workgroup one or two row
-// blocks: the Ab partials of K_{t-1}, the Onsager residual, the z^2 partial),
-// publishes its rows of z_t write-through (sc1 stores, every storing wave's
-// vmcnt(0), a workgroup barrier, one agent-scope add to an arrival counter),
-// waits for every workgroup's arrival, and only then stages z_t: the bucket
-// and Ab-table loads of iteration t, which do not depend on z, are in flight
-// during the row step.  z is double-buffered (K_t reads z_{t-1} from one
-// buffer and writes z_t to the other), so no XCD's L2 can hold a line of the
-// buffer the section phase reads from before the hand-off; after it, z_t and
-// the z^2 partials are read with sc1 loads (MI355X_MICROARCH.md, hand-off
-// forms).  The sums are k_row2<R>'s, in k_row2's order: bit for bit the
-// two-kernel path (tests/test_gpu_fused.py).
-// Measured: SLOWER than two launches, c2 1161-1168 against
-// 1367-1396 codewords/s: the hand-off (write-through stores drained, 256
-// arrivals, the poll) takes ~3.3 us where a kernel boundary takes ~1.7, and
-// the row step's loads share the first round trip with the tables.  Kept
-// opt-in (SPARC_AMP_FUSE=1) as the measured alternative; never the default.
-template <typename real>
-struct FuseArgs {
-  RowArgs<real> r;   // row step t-1 in k_row2's meaning: r.t = t-1, r.z_in = z_{t-1}, r.z = z_t (out)
-  unsigned* bar;     // arrival counters: 8, 32 words (128 B) apart, summed by the poll
-  int* err;          // set to 1 when the arrival poll gives up (never expected: a hang guard)
-  unsigned target;   // counter sum once every workgroup of this launch has arrived
-  int NB;            // row blocks of R rows (workgroup g: blocks g and g + gridDim.x)
-};
-
-constexpr int kBarSpinLimit = 1 << 20;  // ~0.1 s of polling, then err and go on
-
-// k_row2<R, 512>'s loads, sums and finish for the (up to) two row blocks of
-// this workgroup: threads 0..511, thread (rl, pg) sums partials pg + NG u of
-// row rl in order, the NG group sums are added in group order by wave 0
-// (first block) / wave 1 (second block).
-template <typename real, int R>
-struct FusedRows {
-  static constexpr int NG = 512 / R, U = 256 / NG;  // G <= 256 partials (host-checked)
-  real t[2][U];
-  real yv, zv, bbv[4], tau, last;
-  int blk0, blk1;  // this workgroup's blocks, or -1 (NB may be below or above the workgroup count)
-  __device__ __forceinline__ void issue(const FuseArgs<real>& f, int tid) {
-    const RowArgs<real>& a = f.r;
-    const int rl = tid & (R - 1), pg = (tid / R) % NG;
-    blk0 = (int)blockIdx.x < f.NB ? (int)blockIdx.x : -1;
-    blk1 = blockIdx.x + gridDim.x < f.NB ? blockIdx.x + gridDim.x : -1;
-    tau = ld_vmem(a.tau + a.t);
-    last = a.t > 0 ? ld_vmem(a.tau + a.t - 1) : (real)0;
-    const int wv = tid >> 6, lane = tid & 63;
-    yv = zv = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bbv[q] = 0;
-    if (wv < 2) {  // wave w finishes block w (loads clamped to block 0 where it has none)
-      const int blk = (wv == 1 && blk1 >= 0) ? blk1 : (blk0 >= 0 ? blk0 : 0);
-      const int r = blk * R + (lane & (R - 1));
-      const int o = r < a.n ? r : 0;
-      yv = a.y[o];
-      zv = a.z_in[o];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bbv[q] = lane + 64 * q < a.Gb ? a.bbp[lane + 64 * q] : (real)0;
-    }
-    if (tid < 512) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int blk = (k == 1 && blk1 >= 0) ? blk1 : (blk0 >= 0 ? blk0 : 0);
-        const real* p = a.abp + (size_t)blk * a.G * R + rl;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int g = pg + NG * u;
-          t[k][u] = p[(size_t)(g < a.G ? g : pg) * R];
-        }
-      }
-    }
-  }
-  // returns false when the row step is stopped (tau_{t-1} == tau_{t-2}: nothing
-  // changes, no hand-off is needed and the section phase stops as well)
-  __device__ __forceinline__ bool finish(const FuseArgs<real>& f, int tid, real* red) {
-    const RowArgs<real>& a = f.r;
-    if (a.early_stop && tau == last) return false;  // uniform over the grid
-    const real tau2 = tau * tau;
-    const int rl = tid & (R - 1), pg = tid / R;
-    if (tid < 512) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        real acc = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (pg + NG * u < a.G) acc += t[k][u];
-        red[(k * NG + pg) * (R + 1) + rl] = acc;
-      }
-    }
-    __syncthreads();
-    const int wv = tid >> 6, lane = tid & 63;
-    if ((wv == 0 && blk0 >= 0) || (wv == 1 && blk1 >= 0)) {
-      const int blk = wv == 1 ? blk1 : blk0;
-      real sacc = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sacc += bbv[q];
-      const real bb = wave_sum(sacc);
-      const real ons = a.Pb[0] - bb / (real)a.n;
-      const int r = blk * R + (lane & (R - 1));
-      real zn = 0;
-      if (lane < R && r < a.n) {
-        real acc = 0;
-#pragma unroll
-        for (int q = 0; q < NG; ++q) acc += red[(wv * NG + q) * (R + 1) + rl];
-        const real ab = acc / a.sqrt_n;
-        zn = yv - ab;
-        zn += (zv / tau2) * ons;
-        __hip_atomic_store(a.z + r, zn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: write-through
-      }
-      const real sz = wave_sum(zn * zn);
-      if (lane == 0) __hip_atomic_store(a.zzp + blk, sz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its stores are done
-    }
-    __syncthreads();
-    return true;
-  }
-};
-
-// Arrival of this workgroup and the wait for all of them (one lane polls the
-// eight counters with sc1 loads, s_sleep between polls, bounded).
-template <typename real>
-__device__ __forceinline__ void grid_arrive_wait(const FuseArgs<real>& f, int tid) {
-  if (tid == 0) {
-    __hip_atomic_fetch_add(f.bar + (blockIdx.x & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int spin = 0;; ++spin) {
-      unsigned s = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s += __hip_atomic_load(f.bar + i * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s >= f.target) break;
-      if (spin >= kBarSpinLimit) {
-        __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-}
-
-// FR > 0: the fused kernel (row step of t-1 on FR-row blocks first, see
-// FuseArgs); FR = 0: the section kernel alone.
-// IB: the bucket tables of the workgroup's sections are built in LDS from the
-// ordering values (fwo2 / fwo3: n entries per section, which also give the Ab
-// rows their bucket and sign) instead of loading the w-entry bucket tables
-// and the Ab table: the first memory round trip carries z, the z^2 partials,
-// beta and the ordering values (C2: 18 KB per workgroup instead of 32 + 18 KB
-// over two trips); the tables are filled with the zero slot n while it is in
-// flight, then every row r is written to slot o_l(r) of its sections' tables
-// (ds_write_b16) and the gather reads the tables from LDS.  The same entries
-// as the bucket table in HBM, visited in the same order: bit-identical results.
-template <typename real, int EQ, int QW, int SPW = 2, int FR = 0, bool IB = false>
-__device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs<real>* fu = nullptr) {
+// The pair / triple section kernels' body (SPW sections x QW waves).
+template <typename real, int EQ, int QW, int SPW = 2>
+__device__ __forceinline__ void secq_body(const SecArgs<real>& a) {
   static_assert(SPW == 2 || SPW == 3, "sections per workgroup");
-  static_assert(!IB || FR == 0, "the fused kernels load the bucket tables from HBM");
   STAMP(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = SPW * QW * 64;
   // bucket h-steps whose table loads are in flight together: triples take 8
   // (C4, 32 h-steps: half the first round trip's table bytes, the rest lands
   // during the gather; 961 -> 996 cw/s), pairs 16 (c2: all 16 up front; 8 neutral)
-#ifndef SA_KH3
-#define SA_KH3 8
-#endif
-  constexpr int KH = EQ >= 8 ? 4 : (SPW == 3 ? SA_KH3 : 16);
+  constexpr int KH = EQ >= 8 ? 4 : (SPW == 3 ? 8 : 16);
   constexpr int NQ = (EQ + 3) / 4;
   // rows per thread per pass, all Ab-table loads issued with the first loads: n <= 4608 (pairs,
   // C2) / 8448 (triples, C4 n = 8294) in one pass (a second pass reloads the table mid-phase:
@@ -1672,21 +1494,17 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   real* ts = zs + zslots;          // [SPW][M]   T_l = H_M beta_l
   real* xb = ts + SPW * M;         // [SPW][M]   top-stage exchange, one M per section
   real* red = xb + SPW * M;        // [SPW*QW][4] per-wave max, S, S2, beta^2
-  uint16_t* invs = reinterpret_cast<uint16_t*>(red + SPW * QW * 4);  // IB: [SPW][w] bucket tables (16-B aligned)
 
   real v[EQ];
   real bprev[EQ];
   const real* bl = a.beta + (size_t)b * LM + (size_t)lc * M + eoff;
   real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M + eoff;
-  const uint16_t* il = IB ? invs + sidx * a.w + eoff : a.inv + (size_t)lc * a.w + eoff;
   // the HBM bucket tables as a workgroup-uniform base + this wave's 32-bit offset
   const uint16_t* ibase = a.inv + (size_t)g * SPW * a.w;
   const unsigned ioff = (unsigned)((lc - g * SPW) * a.w + eoff);
   const uint32_t* fw = (SPW == 2 ? a.fwd2 : a.fwd3) + (size_t)g * n;
   ushort4 tb[KH][NQ];
-  // Ab-table entries of this thread's rows; IB: the ordering values (triples: two words)
-  using FO = typename std::conditional<IB && SPW == 3, uint2, uint32_t>::type;
-  FO f[KR];
+  uint32_t f[KR];  // Ab-table entries of this thread's rows
 
   // Load order: z's LDS-DMA first, then the z^2 partials and tau_{t-1}, then
   // the tables, all unconditional (straight-line).  While an LDS-DMA is in
@@ -1701,60 +1519,14 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   // z^2 partials held in registers: k_row2 writes ceil(n / 32) (C4 n = 8294:
   // 260, past the 256 of K = 4, whose fallback re-reads them: one more memory
   // round trip before tau), k_row2<16> ceil(n / 16) (C2: 288)
-#ifndef SA_ZZK
-#define SA_ZZK 5
-#endif
-  ZZParts<real, SA_ZZK> zz;
-  bool dma;
-  real last, cl;
-  if constexpr (FR > 0) {
-    // row step t-1 first; the tables of iteration t (independent of z) and
-    // the previous beta are issued right behind its loads and land under it
-    FusedRows<real, FR> fr;
-    fr.issue(*fu, tid);
-    load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);
-    load_section<real, EQ>(bl, bprev, lane, Mq);
-    cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
-#pragma unroll
-    for (int u = 0; u < KR; ++u) {  // the Ab-table rows too (unconditional, clamped)
-      const int r = u * NT + tid;
-      f[u] = fw[r < n ? r : 0];
-    }
-    const bool ran = fr.finish(*fu, tid, reinterpret_cast<real*>(smem));
-    STAMP(11);
-    if (ran) grid_arrive_wait(*fu, tid);
-    STAMP(12);
-    // z_t and the z^2 partials: published in this launch, read with sc1 loads
-    dma = stage_z_dma<real, NT, kAuxSc1>(zb, zs, n, tid);  // host-checked: z is 16-B aligned
-    zz.template issue<true>(zzb, a.NZ, lane);
-    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
-  } else {
-    dma = stage_z_dma<real, NT>(zb, zs, n, tid);
-    if (!dma) zst.issue(zb, n, tid);
-    zz.issue(zzb, a.NZ, lane);
-    last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
-    if constexpr (IB) {
-      // the ordering values of this thread's rows (one pass: host-checked n <= NT * KR)
-      if constexpr (SPW == 2) {
-        const uint32_t* fo = a.fwo2 + (size_t)g * n;
-#pragma unroll
-        for (int u = 0; u < KR; ++u) { const int r = u * NT + tid; f[u] = fo[r < n ? r : 0]; }
-      } else {
-        const uint2* fo = a.fwo3 + (size_t)g * n;
-#pragma unroll
-        for (int u = 0; u < KR; ++u) { const int r = u * NT + tid; f[u] = fo[r < n ? r : 0]; }
-      }
-    } else {
-      load_buckets_off<EQ, KH>(ibase, ioff, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
-    }
-    load_section<real, EQ>(bl, bprev, lane, Mq);
-    cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
-    if constexpr (IB) {  // every slot empty (the zero slot n) while the loads are in flight
-      const uint32_t nn = (uint32_t)n | ((uint32_t)n << 16);
-      uint4* iv = reinterpret_cast<uint4*>(invs);
-      for (int i = tid; i < SPW * a.w / 8; i += NT) iv[i] = make_uint4(nn, nn, nn, nn);
-    }
-  }
+  ZZParts<real, 5> zz;
+  const bool dma = stage_z_dma<real, NT>(zb, zs, n, tid);
+  if (!dma) zst.issue(zb, n, tid);
+  zz.issue(zzb, a.NZ, lane);
+  const real last = a.t > 0 ? ld_vmem(a.tau + (size_t)b * a.T1 + a.t - 1) : (real)0;
+  load_buckets_off<EQ, KH>(ibase, ioff, 0, a.nhi, M, lane, tb);  // bucket stride M; lane elements < Mq
+  load_section<real, EQ>(bl, bprev, lane, Mq);
+  const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
   const real tau = zz.tau(zzb, a.NZ, n);
   const bool stop = a.early_stop && (tau == last);
   if (g == 0 && tid == 0) {
@@ -1772,45 +1544,19 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   const real kk = cl / tau2;
   STAMP(1);
   if (!dma) zst.store(zs, zb, n, tid);
-  else finish_z_dma<real, (FR > 0)>(zb, zs, n, tid);
+  else finish_z_dma<real>(zb, zs, n, tid);
   __syncthreads();
   STAMP(2);
 #ifdef SA_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // diagnostic: table loads landed
   STAMP(10);
 #endif
-  if constexpr (IB) {
-    // row r into slot o_l(r) of each of the workgroup's sections (values in
-    // [1, w), distinct per section; a missing section keeps its empty table)
-    const int w = a.w;
-#pragma unroll
-    for (int u = 0; u < KR; ++u) {
-      const int r = u * NT + tid;
-      if (r < n) {
-        if constexpr (SPW == 2) {
-          invs[f[u] & 0xffffu] = (uint16_t)r;
-          if (g * 2 + 1 < a.L) invs[w + (f[u] >> 16)] = (uint16_t)r;
-        } else {
-          invs[f[u].x & 0xffffu] = (uint16_t)r;
-          if (g * 3 + 1 < a.L) invs[w + (f[u].x >> 16)] = (uint16_t)r;
-          if (g * 3 + 2 < a.L) invs[2 * w + f[u].y] = (uint16_t)r;
-        }
-      }
-    }
-    __syncthreads();
-    STAMP(13);
-    load_buckets<EQ, KH>(il, 0, a.nhi, M, lane, tb);  // from LDS
-  }
-
 #pragma unroll
   for (int i = 0; i < EQ; ++i) v[i] = 0;
   for (int h0 = 0; h0 < a.nhi; h0 += KH) {
     ushort4 tn[KH][NQ];
     const bool more = h0 + KH < a.nhi;
-    if (more) {
-      if constexpr (IB) load_buckets<EQ, KH>(il, h0 + KH, a.nhi, M, lane, tn);
-      else load_buckets_off<EQ, KH>(ibase, ioff, h0 + KH, a.nhi, M, lane, tn);
-    }
+    if (more) load_buckets_off<EQ, KH>(ibase, ioff, h0 + KH, a.nhi, M, lane, tn);
     gather_buckets<real, EQ, KH>(zs, h0, a.nhi, tb, v);
     if (more) {
 #pragma unroll
@@ -1825,12 +1571,10 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   // flight, instead of adding their bytes (C2 18 KB, C4 33 KB per workgroup)
   // to the first memory round trip, which every wave waits for (C4 single
   // codeword 860 -> 894 cw/s, c2 1378 -> 1394; `k_sec43` 11.0 -> 10.7 us)
-  if constexpr (FR == 0 && !IB) {
 #pragma unroll
-    for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
-      const int r = u * NT + tid;
-      f[u] = ld_off(fw, (unsigned)(r < n ? r : 0) * 4u);  // uniform base + 32-bit offset
-    }
+  for (int u = 0; u < KR; ++u) {  // unconditional (clamped): see load_section
+    const int r = u * NT + tid;
+    f[u] = ld_off(fw, (unsigned)(r < n ? r : 0) * 4u);  // uniform base + 32-bit offset
   }
   STAMP(3);
   fwht_wave<real, EQ>(v, lane, 64);
@@ -1900,46 +1644,22 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
   const int smask = (int)((1u << sh) - 1u);
   static_assert(NT % 32 == 0, "a pass of rows is a whole number of row blocks");
   const size_t ustep = sh < 31 ? (size_t)(NT >> sh) * gstride : (size_t)NT;
-#ifdef SA_DIAG_ROWS_NOSTORE
-  real diag_sink = 0;
-#endif
   for (int r0 = 0; r0 < n; r0 += NT * KR) {
-    if constexpr (!IB) {
-      if (r0 > 0) {  // n > NT * KR only
+    if (r0 > 0) {  // n > NT * KR only
 #pragma unroll
-        for (int u = 0; u < KR; ++u) {
-          const int r = r0 + u * NT + tid;
-          f[u] = fw[r < n ? r : 0];
-        }
+      for (int u = 0; u < KR; ++u) {
+        const int r = r0 + u * NT + tid;
+        f[u] = fw[r < n ? r : 0];
       }
     }
     real* const pbase = sbase + (size_t)((r0 + tid) >> sh) * gstride + ((r0 + tid) & smask);
     // row r's term of the pair (triple) and its store
     auto row = [&](int u, int r) {
       real t;
-      if constexpr (IB) {
-        // bucket o & (M-1), sign parity(o >> log2 M): the Ab-table entry of the ordering value
-        const int lgM = 31 - __clz(M);
-        auto term = [&](uint32_t o, int sec) {
-          const real v0 = ts[sec * M + (o & (uint32_t)(M - 1))];
-          return (__popc(o >> lgM) & 1) ? -v0 : v0;
-        };
-        if constexpr (SPW == 2) {
-          t = term(f[u] & 0xffffu, 0);
-          t += term(f[u] >> 16, 1);
-        } else {
-          t = term(f[u].x & 0xffffu, 0);
-          t += term(f[u].x >> 16, 1);
-          t += term(f[u].y, 2);
-        }
-      } else if constexpr (SPW == 2) {
+      if constexpr (SPW == 2) {
         const uint32_t e = f[u];
-#ifdef SA_DIAG_ROWS_NOLDS  // diagnostic (stamps builds): no LDS reads in the Ab rows, wrong results
-        const real v0 = (real)(e & 0xffu), v1 = (real)((e >> 16) & 0xffu);
-#else
         const real v0 = ts[e & 0x7fffu];
         const real v1 = ts[M + ((e >> 16) & 0x7fffu)];
-#endif
         t = (e & 0x8000u) ? -v0 : v0;
         t += (e & 0x80000000u) ? -v1 : v1;
       } else {
@@ -1951,16 +1671,12 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
         t += (e & 0x80000u) ? -v1 : v1;
         t += (e & 0x20000000u) ? -v2 : v2;
       }
-#ifdef SA_DIAG_ROWS_NOSTORE  // diagnostic (stamps builds): one store per thread instead of one per row
-      diag_sink += t;
-#else
       // one branch-free store for both layouts ([G][n] is the row-block form
       // with sh = 31); triples: row r0 + tid + u NT at pbase + u ustep (NT is
       // a whole number of 16- / 32-row blocks; pairs measured faster with the
       // address from r)
       if constexpr (SPW == 3) st_part(pbase + u * ustep, t);
       else st_part(&sbase[(size_t)(r >> sh) * gstride + (r & smask)], t);
-#endif
     };
     if (r0 + NT * KR <= n) {
       // uniform: every row of the pass exists; no per-row branch, so the
@@ -1975,9 +1691,6 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
       }
     }
   }
-#ifdef SA_DIAG_ROWS_NOSTORE
-  st_part(&abp[tid], diag_sink);
-#endif
 #ifdef SA_STAMPS
   STAMP(8);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1985,21 +1698,12 @@ __device__ __forceinline__ void secq_body(const SecArgs<real>& a, const FuseArgs
 #endif
 }
 
-template <typename real, int E4, bool IB = false>
-__global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) { secq_body<real, E4, 4, 2, 0, IB>(a); }
+template <typename real, int E4>
+__global__ void __launch_bounds__(512) k_sec4(SecArgs<real> a) { secq_body<real, E4, 4, 2>(a); }
 // Three sections per workgroup (12 waves): L = 3 x CUs (L = 768 on 256 CUs)
 // puts one workgroup on every CU where pairs leave half the CUs with two.
-template <typename real, int E4, bool IB = false>
-__global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real, E4, 4, 3, 0, IB>(a); }
-// The fused kernels (row step of t-1, hand-off, section step of t)
-template <typename real, int E4, int FR>
-__global__ void __launch_bounds__(512) k_sec4f(SecArgs<real> a, FuseArgs<real> f) {
-  secq_body<real, E4, 4, 2, FR>(a, &f);
-}
-template <typename real, int E4, int FR>
-__global__ void __launch_bounds__(768) k_sec43f(SecArgs<real> a, FuseArgs<real> f) {
-  secq_body<real, E4, 4, 3, FR>(a, &f);
-}
+template <typename real, int E4>
+__global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real, E4, 4, 3>(a); }
 // ---------------------------------------------------------------------------
 // Batched section kernel (B codewords share the operator)
 // ---------------------------------------------------------------------------
@@ -2092,10 +1796,6 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
   // this kernel (it declares no static LDS: checked on the host at context
   // creation), so the scaled row index is the LDS address itself.
   (void)zsb;
-#ifdef SA_FAKE_GATHER  // diagnostic: conflict-free consecutive addresses (wrong results, timing only)
-#pragma unroll
-  for (int i = 0; i < E; ++i) ad[i] = ((threadIdx.x & 63) + 64 * i) << SH;
-#endif
   using V = real __attribute__((ext_vector_type(CB)));
   using lds_v = __attribute__((address_space(3))) const V;
   real zz[E][CB];
@@ -2150,17 +1850,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     const int bid = blockIdx.x, total = a.G * a.NC;
     if ((a.G & 7) == 0 && (total & 7) == 0) {
       const int x = bid & 7, j = bid >> 3;
-#ifndef SA_SECB_CHUNK_FAST
       // the XCD's G/8 section groups fastest: the workgroups in flight on
       // one XCD (two per CU) cover G/8 groups' tables and a few codeword
       // chunks' z, which stay in its L2 together
       const int gx = a.G >> 3;
       g = (j % gx) * 8 + x;
       chunk = j / gx;
-#else
-      g = (j / a.NC) * 8 + x;
-      chunk = j % a.NC;
-#endif
     } else {
       g = bid / a.NC;
       chunk = bid % a.NC;
@@ -2476,11 +2171,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
           if constexpr (sizeof(real) == 4) {
             // binary32: k and the LDS byte address in two ops, the sign
             // bit ORed into 1.0f (one op for the upper half-word)
-#ifdef SA_FAKE_ROWS  // diagnostic: conflict-free consecutive T reads (wrong results, timing only)
-            const unsigned k = ((unsigned)(threadIdx.x & 63) + 64u * s4 + (unsigned)(wd & 1u)) & (unsigned)(M - 1);
-#else
             const unsigned k = up ? __builtin_amdgcn_ubfe(wd, 16, 15) : (wd & 0x7fffu);
-#endif
             const unsigned sb = (up ? wd : wd << 16) & 0x80000000u;
             sg = __uint_as_float(sb | 0x3f800000u);
             using V = real __attribute__((ext_vector_type(CB)));
@@ -2863,10 +2554,11 @@ __global__ void __launch_bounds__(NT) k_row2(RowArgs<real> a) {
                          : a.abp + (size_t)b * a.G * n + (r < n ? r : 0);
     real acc = 0;
     constexpr int U = 256 / NG;  // G = 256 (C2, C4): every load of a thread in one pass
-    if ((R == 16 || (a.pt && sizeof(real) == 4)) && a.G == NG * U) {
-      // row-block-major partials (16-row blocks always are) with exactly NG x U
-      // partials (32-row blocks: binary32 only, C4 single codeword +1 %; the
-      // binary64 32-row blocks measured 1.4 % slower in this form):
+    if (a.pt && (R == 16 || sizeof(real) == 4) && a.G == NG * U) {
+      // row-block-major partials with exactly NG x U partials (32-row blocks:
+      // binary32 only, C4 single codeword +1 %; the binary64 32-row blocks
+      // measured 1.4 % slower in this form).  The [G][n] partials of k_sec
+      // (sa_Ab, the beta0 start) take the general loop even in 16-row blocks:
       // constant strides from the block base, no bounds, 32-bit offsets (the
       // general form spent ~40 VALU ops of 64-bit address math before the
       // first load); the same loads and sums in the same order
@@ -2974,12 +2666,6 @@ __global__ void k_fill32(uint32_t* p, uint32_t v, size_t nw) {
 // Fused path: the final residual of a codeword lies in the buffer of parity
 // iters[b] (z double-buffered); bring it home to z (one codeword).
 template <typename real>
-__global__ void k_z_final(real* z, const real* z2, const int* it, int n) {
-  if (!(it[0] & 1)) return;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) z[i] = z2[i];
-}
-
-template <typename real>
 __global__ void k_beta_final(real* beta, const real* beta2, const int* it, size_t LM) {
   const int b = blockIdx.y;
   if (!(it[b] & 1)) return;
@@ -3014,120 +2700,176 @@ __global__ void k_dense_build(const uint32_t* ord, float* A, int L, int M, int n
   }
 }
 
+// 16-byte vectors of the dense kernels: 4 binary32 or 2 binary64 elements
+template <typename real> struct V16;
+template <> struct V16<float> { using t = f4; static constexpr int N = 4; };
+template <> struct V16<double> { using t = double __attribute__((ext_vector_type(2))); static constexpr int N = 2; };
+
+// Streaming (non-temporal) 16-B load of the design matrix: read once per pass.
+template <typename real>
+__device__ __forceinline__ typename V16<real>::t ld_stream_v(const real* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const typename V16<real>::t*>(p));
+}
+
+template <typename real>
 struct DenseArgs {
-  const float* A;     // [n][lda]
-  const float* z;     // [B][n]
-  float* azp;         // [B][RS][lda]    Az partials (unscaled by 1/sqrt(n): A holds it)
-  const float* beta;  // [B][L*M]
-  float* abp;         // [B][KS][n]      Ab partials
-  const float* zzp;   // [B][NZ]
-  const float* tau;   // [B][T1]
+  const real* A;      // [n][lda]
+  const real* z;      // [B][n]
+  real* azp;          // [B][RS][lda]    Az partials (A carries any 1/sqrt(n))
+  const real* beta;   // [B][L*M]
+  real* abp;          // [B][KS][n]      Ab partials
+  const real* zzp;    // [B][NZ]
+  const real* tau;    // [B][T1]
   int L, M, n, NZ, T1, t, early_stop, RS, KS, mode;  // mode: 0 = AMP stop test, 1 = none
   size_t lda;
 };
 
-__device__ __forceinline__ bool dense_stopped(const DenseArgs& a, int b) {
+template <typename real>
+__device__ __forceinline__ bool dense_stopped(const DenseArgs<real>& a, int b) {
   if (a.mode != 0 || !a.early_stop) return false;
-  const float tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, a.n);
-  const float last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : 0.f;
+  const real tau = tau_from_parts(a.zzp + (size_t)b * a.NZ, a.NZ, a.n);
+  const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
   return tau == last;
 }
 
 // Az partials: azp[b][rs][j] = sum_{r in split rs} A[r][j] z[b][r].
-// 256 threads x 4 columns (16-B loads) per workgroup; rows split RS ways.
-__global__ void __launch_bounds__(256) k_dense_az(DenseArgs a) {
-  __shared__ float zsh[2048];
+// 256 threads x one 16-B column vector (4 binary32 / 2 binary64 columns) per
+// workgroup; rows split RS ways; row order within a split.
+template <typename real>
+__global__ void __launch_bounds__(256) k_dense_az(DenseArgs<real> a) {
+  constexpr int N = V16<real>::N;
+  __shared__ real zsh[2048];
   const int b = blockIdx.z, rs = blockIdx.y;
   if (dense_stopped(a, b)) return;
   const int rows_per = (a.n + a.RS - 1) / a.RS;
   const int r0 = rs * rows_per, r1 = min(a.n, r0 + rows_per);
-  const size_t j = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const size_t j = ((size_t)blockIdx.x * 256 + threadIdx.x) * N;
+  real acc[N];
+#pragma unroll
+  for (int q = 0; q < N; ++q) acc[q] = 0;
   for (int rb = r0; rb < r1; rb += 2048) {
     const int cnt = min(2048, r1 - rb);
     __syncthreads();
     for (int i = threadIdx.x; i < cnt; i += 256) zsh[i] = a.z[(size_t)b * a.n + rb + i];
     __syncthreads();
     if (j < a.lda) {
-      const float* Ap = a.A + (size_t)rb * a.lda + j;
+      const real* Ap = a.A + (size_t)rb * a.lda + j;
       int i = 0;
       for (; i + 8 <= cnt; i += 8) {
-        float4 v[8];
+        typename V16<real>::t v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld_stream(Ap + (size_t)(i + u) * a.lda);
+        for (int u = 0; u < 8; ++u) v[u] = ld_stream_v<real>(Ap + (size_t)(i + u) * a.lda);
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const float zz = zsh[i + u];
-          acc.x += v[u].x * zz; acc.y += v[u].y * zz; acc.z += v[u].z * zz; acc.w += v[u].w * zz;
+          const real zz = zsh[i + u];
+#pragma unroll
+          for (int q = 0; q < N; ++q) acc[q] += v[u][q] * zz;
         }
       }
       for (; i < cnt; ++i) {
-        const float4 v = *reinterpret_cast<const float4*>(Ap + (size_t)i * a.lda);
-        const float zz = zsh[i];
-        acc.x += v.x * zz; acc.y += v.y * zz; acc.z += v.z * zz; acc.w += v.w * zz;
+        const typename V16<real>::t v = *reinterpret_cast<const typename V16<real>::t*>(Ap + (size_t)i * a.lda);
+        const real zz = zsh[i];
+#pragma unroll
+        for (int q = 0; q < N; ++q) acc[q] += v[q] * zz;
       }
     }
   }
-  if (j < a.lda)
-    *reinterpret_cast<float4*>(a.azp + ((size_t)b * a.RS + rs) * a.lda + j) = acc;
+  if (j < a.lda) {
+    typename V16<real>::t o;
+#pragma unroll
+    for (int q = 0; q < N; ++q) o[q] = acc[q];
+    *reinterpret_cast<typename V16<real>::t*>(a.azp + ((size_t)b * a.RS + rs) * a.lda + j) = o;
+  }
 }
 
 // Ab partials: abp[b][ks][r] = sum_{j in split ks} A[r][j] beta[b][j];
 // 8 rows per workgroup share each 16-B beta load.
 constexpr int kDenseRows = 8;
-__global__ void __launch_bounds__(256) k_dense_ab(DenseArgs a, const float* tau) {
-  __shared__ float red[kDenseRows][4];
+template <typename real>
+__global__ void __launch_bounds__(256) k_dense_ab(DenseArgs<real> a, const real* tau) {
+  constexpr int N = V16<real>::N;
+  __shared__ real red[kDenseRows][4];
   const int b = blockIdx.z, ks = blockIdx.y;
   if (a.mode == 0 && a.early_stop) {
-    const float t0 = tau[(size_t)b * a.T1 + a.t];
-    const float t1 = a.t > 0 ? tau[(size_t)b * a.T1 + a.t - 1] : 0.f;
+    const real t0 = tau[(size_t)b * a.T1 + a.t];
+    const real t1 = a.t > 0 ? tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
     if (t0 == t1) return;
   }
   const int r0 = blockIdx.x * kDenseRows;
   const size_t LM = (size_t)a.L * a.M;
-  const size_t n4 = (LM + 3) / 4;  // float4 columns with data (pad columns are 0 in A)
-  const size_t per = (n4 + a.KS - 1) / a.KS;
-  const size_t c0 = ks * per, c1 = c0 + per < n4 ? c0 + per : n4;
-  float acc[kDenseRows];
+  const size_t nv = (LM + N - 1) / N;  // 16-B column vectors with data (pad columns are 0 in A)
+  const size_t per = (nv + a.KS - 1) / a.KS;
+  const size_t c0 = ks * per, c1 = c0 + per < nv ? c0 + per : nv;
+  real acc[kDenseRows];
 #pragma unroll
-  for (int k = 0; k < kDenseRows; ++k) acc[k] = 0.f;
-  const float* bb = a.beta + (size_t)b * LM;
+  for (int k = 0; k < kDenseRows; ++k) acc[k] = 0;
+  const real* bb = a.beta + (size_t)b * LM;
   for (size_t c = c0 + threadIdx.x; c < c1; c += 256) {
-    float4 bv;
-    if (c * 4 + 3 < LM) {
-      bv = *reinterpret_cast<const float4*>(bb + c * 4);
+    real bv[N];
+    if (c * N + N - 1 < LM && ((LM % N) == 0)) {
+      const typename V16<real>::t t = *reinterpret_cast<const typename V16<real>::t*>(bb + c * N);
+#pragma unroll
+      for (int q = 0; q < N; ++q) bv[q] = t[q];
     } else {
-      bv.x = c * 4 + 0 < LM ? bb[c * 4 + 0] : 0.f;
-      bv.y = c * 4 + 1 < LM ? bb[c * 4 + 1] : 0.f;
-      bv.z = c * 4 + 2 < LM ? bb[c * 4 + 2] : 0.f;
-      bv.w = 0.f;
+#pragma unroll
+      for (int q = 0; q < N; ++q) bv[q] = c * N + q < LM ? bb[c * N + q] : (real)0;
     }
 #pragma unroll
     for (int k = 0; k < kDenseRows; ++k) {
       const int r = r0 + k;
       if (r < a.n) {
-        const float4 v = ld_stream(a.A + (size_t)r * a.lda + c * 4);
-        acc[k] += v.x * bv.x + v.y * bv.y + v.z * bv.z + v.w * bv.w;
+        const typename V16<real>::t v = ld_stream_v<real>(a.A + (size_t)r * a.lda + c * N);
+        real d = v[0] * bv[0];
+#pragma unroll
+        for (int q = 1; q < N; ++q) d += v[q] * bv[q];
+        acc[k] += d;
       }
     }
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < kDenseRows; ++k) {
-    const float s = wave_sum(acc[k]);
+    const real s = wave_sum(acc[k]);
     if (lane == 0) red[k][wv] = s;
   }
   __syncthreads();
   if (threadIdx.x < kDenseRows) {
     const int r = r0 + threadIdx.x;
     if (r < a.n) {
-      const float s = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+      const real s = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
       a.abp[((size_t)b * a.KS + ks) * a.n + r] = s;
     }
   }
 }
 
+// Dense Az partial reduction into d_out (B x L*M), used by sa_Az on the dense backends.
+template <typename real>
+__global__ void k_dense_az_reduce(const real* azp, real* out, int RS, size_t lda, size_t LM, int B) {
+  const size_t total = (size_t)B * LM;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = i / LM, j = i % LM;
+    real s = 0;
+    for (int rs = 0; rs < RS; ++rs) s += azp[(b * RS + rs) * lda + j];
+    out[i] = s;
+  }
+}
+
+// A caller's matrix (SA_BACKEND_MATRIX): rows [r0, r0 + rows) of the fp64
+// host matrix (staged, [rows][LM]) into the device matrix [np][lda] in the
+// context precision, pad columns zero.
+template <typename real>
+__global__ void k_matrix_rows(const double* __restrict__ src, real* __restrict__ A, long long rows, long long LM,
+                              size_t lda, long long r0) {
+  const long long total = rows * (long long)lda;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / (long long)lda, j = i % (long long)lda;
+    A[(size_t)(r0 + r) * lda + j] = j < LM ? (real)src[r * LM + j] : (real)0;
+  }
+}
+
 #include "dense_i8.hip"
+#include "dense_mfma.hip"
 
 // Dense-path denoiser: sums the RS Az partials of one section (wave) and
 // applies denoise_section; writes tau (workgroup 0) and beta^2 partials.
@@ -3275,6 +3017,7 @@ enum { K_SEC = 0, K_ROW = 1, K_DAZ = 2, K_DDEN = 3, K_DAB = 4, K_QNT = 5, K_NKIN
 struct sa_ctx {
   Prof* prof = nullptr;
   int L = 0, M = 0, n = 0, w = 0, nhi = 0, backend = 0, prec = 0, device = 0;
+  int plan = 0;       // SA_PLAN_* options of sa_create_ex (0: every choice by the built-in rules)
   bool pow2 = true;  // M a power of two (the Hadamard kernels, bit-level glue)
   int G = 0, NZ = 0, E = 1;
   int n_cus = 256;
@@ -3292,21 +3035,9 @@ struct sa_ctx {
   bool pt_on = false;  // row-block-major Ab partials between k_sec4 / k_sec43 and k_row2 (SecArgs::pt)
   bool sec4 = false;   // k_sec4 (4 waves per section) fits and is chosen
   size_t sec4_lds = 0;
-  // bucket tables built in LDS from the ordering values (k_sec4 / k_sec43 <IB>):
-  // the section kernel loads fwo2 / fwo3 (n entries per section) instead of the
-  // w-entry bucket table plus the Ab table; sec4_lds / sec3_lds include the
-  // LDS image of the bucket tables
-  bool ib = false;
-  uint32_t* d_fwo2 = nullptr;
-  uint2* d_fwo3 = nullptr;
   int NZ16 = 0;        // k_row2 32-row blocks; nz_cur = z^2 partial count of the current decode
   int NZh = 0;         // k_row2 16-row blocks (row16)
   bool row16 = false;  // k_row2<16> after k_sec4 (row-block-major partials, NZh <= 320)
-  bool fuse = false;   // one codeword: the row step of t-1 fused into the section kernel of t (k_sec4f / k_sec43f)
-  void* d_z2 = nullptr;         // the fused path's second residual buffer (z double-buffered)
-  unsigned* d_bar = nullptr;    // the fused path's arrival counters (8 x 128 B)
-  int* d_err = nullptr;         // set by a fused launch whose arrival poll gave up
-  unsigned bar_seq = 0;         // fused launches since the counters were last cleared (host side)
   int NZ4 = 0, NZ2 = 0;  // k_rowv<4> 256-row / k_rowv<2> 128-row blocks
   int row_kind = 0;    // row kernel of the current decode: 0 k_row, 1 k_row2, 2 k_rowv<4>, 3 k_rowv<2>, 4 k_row2<16>, 5 k_rowc
   bool zil_last = false;  // the last decode left z codeword-interleaved ([NC][n][CB], zil_for)
@@ -3320,13 +3051,20 @@ struct sa_ctx {
   bool invb_done = false;
   uint16_t* d_fwd = nullptr;
   uint32_t* d_fwd2 = nullptr;
-  float* d_A = nullptr;
+  void* d_A = nullptr;  // dense [np][lda] design matrix (binary32; SA_BACKEND_MATRIX: the context precision)
   // int8 matrix-core dense path (B >= 4; dense_i8.hip): A8 [np8][LMp8], AT8 [LMp8][np8],
   // digit planes of z [3][Bp8][np8] and beta [3][Bp8][LMp8], per-codeword scales
   int8_t *d_A8 = nullptr, *d_AT8 = nullptr, *d_zq = nullptr, *d_bq = nullptr;
   double *d_zsc = nullptr, *d_bsc0 = nullptr, *d_bfix = nullptr;
   long long np8 = 0, LMp8 = 0;
   int Bp8 = 0;
+  // caller's dense matrix (SA_BACKEND_MATRIX): rows padded to np (a whole
+  // number of 256-row GEMM tiles); for B >= kFMinB codewords (dense_mfma.hip)
+  // its transpose AT [LMy][nk] and the padded GEMM vectors xz [Bcap][nk] (z)
+  // and xb [Bcap][lda] (beta, when L*M is not a whole number of K stages)
+  long long np = 0, nk = 0, LMy = 0;
+  void *d_AT = nullptr, *d_xz = nullptr, *d_xb = nullptr;
+  int fg_cap = 0;
   double cmax = 0;  // max_l sqrt(n Pl_l) of the shared power allocation
   // workspace
   int Bcap = 0, Tcap = 0;
@@ -3385,9 +3123,6 @@ void free_workspace(sa_ctx* c) {
     *p = nullptr;
   }
   dev_free(c->d_iters); c->d_iters = nullptr;
-  dev_free(c->d_z2); c->d_z2 = nullptr;
-  dev_free(c->d_bar); c->d_bar = nullptr;
-  dev_free(c->d_err); c->d_err = nullptr;
   dev_free(c->d_stop); c->d_stop = nullptr;
   dev_free(c->d_idx); c->d_idx = nullptr;
   dev_free(c->d_beta2); c->d_beta2 = nullptr;
@@ -3404,8 +3139,12 @@ constexpr int kI8MinB = 4;    // batches at least this large take the GEMM path
 constexpr int kI8MaxS = 16;   // K splits of the A beta GEMM (its Ab partials)
 
 bool use_i8(const sa_ctx* c, int B) {
-  return c->backend == SA_BACKEND_DENSE && B >= kI8MinB && !getenv("SPARC_AMP_NO_I8");
+  return c->backend == SA_BACKEND_DENSE && B >= kI8MinB;
 }
+
+// the dense backends: a materialised n x (L*M) matrix streamed by GEMVs
+// (the Hadamard design's, or a caller's own: SA_BACKEND_MATRIX)
+bool is_dense(const sa_ctx* c) { return c->backend == SA_BACKEND_DENSE || c->backend == SA_BACKEND_MATRIX; }
 
 int i8_bp(int B) { return (B + kI8TX - 1) / kI8TX * kI8TX; }
 
@@ -3481,10 +3220,16 @@ int ensure_i8(sa_ctx* c, int B) {
   return SA_OK;
 }
 
+int ensure_fgemm(sa_ctx* c, int B);
+
 int ensure_workspace(sa_ctx* c, int B, int T) {
   if (c->backend == SA_BACKEND_DENSE) {
     int rc8 = ensure_i8(c, B > c->Bcap ? B : c->Bcap);
     if (rc8) return rc8;
+  }
+  if (c->backend == SA_BACKEND_MATRIX) {
+    int rcf = ensure_fgemm(c, B > c->Bcap ? B : c->Bcap);
+    if (rcf) return rcf;
   }
   if (B <= c->Bcap && T <= c->Tcap) return SA_OK;
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -3495,6 +3240,7 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   const size_t s = rsz(c), LM = (size_t)c->L * c->M;
   int Gmax = c->G > c->KS ? c->G : c->KS;
   if (c->backend == SA_BACKEND_DENSE && Gmax < kI8MaxS) Gmax = kI8MaxS;
+  if (c->backend == SA_BACKEND_MATRIX && Gmax < kFMaxS) Gmax = kFMaxS;
   if (c->Gb > Gmax) Gmax = c->Gb;
   if (c->G2 > Gmax) Gmax = c->G2;
   if (c->G3 > Gmax) Gmax = c->G3;
@@ -3514,29 +3260,12 @@ int ensure_workspace(sa_ctx* c, int B, int T) {
   if ((rc = dev_alloc(c, (void**)&c->d_idx, (size_t)nB * c->L * sizeof(int32_t)))) return rc;
   if ((rc = dev_alloc(c, &c->d_cb, (size_t)nB * c->L * s))) return rc;
   if ((rc = dev_alloc(c, &c->d_Pb, (size_t)nB * s))) return rc;
-  if ((rc = dev_alloc(c, &c->d_z2, (size_t)c->n * s))) return rc;  // one codeword
-  if ((rc = dev_alloc(c, (void**)&c->d_bar, 8 * 128))) return rc;
-  if ((rc = dev_alloc(c, (void**)&c->d_err, sizeof(int)))) return rc;
-  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
-  if (c->backend == SA_BACKEND_DENSE)
-    if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->RS * c->lda * sizeof(float)))) return rc;
+  if (is_dense(c))
+    if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->RS * c->lda * s))) return rc;
   if (c->backend == SA_BACKEND_HOST)  // the caller's A^T z, one partial per codeword
     if ((rc = dev_alloc(c, &c->d_azp, (size_t)nB * c->lda * s))) return rc;
   c->Bcap = nB;
   c->Tcap = nT;
-  // Debug aid: SPARC_AMP_POISON=<mask> fills the workspace with 0xFF bytes
-  // (NaN) so a read of a value the decode never wrote shows up.
-  if (const char* pz = getenv("SPARC_AMP_POISON")) {
-    const int mask = atoi(pz);
-    const size_t LMs = (size_t)c->L * c->M * s;
-    void* bufs[] = {c->d_y, c->d_z, c->d_beta, c->d_out, c->d_abp, c->d_bbp, c->d_zzp, c->d_tau};
-    const size_t sz[] = {nB * c->n * s, nB * c->n * s, nB * LMs, nB * (LMs > (size_t)c->n * s ? LMs : (size_t)c->n * s),
-                         (size_t)nB * Gmax * ((size_t)c->NZ16 * kRow2Rows) * s, (size_t)nB * Gmax * s,
-                         (size_t)nB * c->NZh * s, (size_t)nB * (nT + 1) * s};
-    for (int i = 0; i < 8; ++i)
-      if (mask & (1 << i)) HIP_TRY(hipMemsetAsync(bufs[i], 0xff, sz[i], c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-  }
   return SA_OK;
 }
 
@@ -3584,7 +3313,6 @@ template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
   a.inv = c->d_inv; a.invb = c->d_invb; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
-  a.fwo2 = c->d_fwo2; a.fwo3 = c->d_fwo3;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
@@ -3700,8 +3428,7 @@ bool use_batched(const sa_ctx* c, int B) { return c->CB > 0 && B >= 4; }
 // Two-waves-per-section kernel for the unbatched path when its G2 x B
 // workgroups fill at least half of the CUs (otherwise k_sec's row splits do).
 bool use_sec2(const sa_ctx* c, int B) {
-  return c->backend == SA_BACKEND_HADAMARD && !use_batched(c, B) && c->G2 > 0 && c->G2 * B * 2 >= c->n_cus &&
-         !getenv("SPARC_AMP_NO_SEC2");
+  return c->backend == SA_BACKEND_HADAMARD && !use_batched(c, B) && c->G2 > 0 && c->G2 * B * 2 >= c->n_cus;
 }
 
 // Ab / beta^2 partials per codeword of the unbatched multi-wave section kernels
@@ -3717,24 +3444,10 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout, int pt =
   dim3 grid(a.G, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
   if (c->sec3) {
-    const size_t lds3 = c->sec3_lds + (c->ib ? 3 * (size_t)c->w * 2 : 0);
-    switch (c->M / 256 + (c->ib ? 2 : 0)) {
-      case 1: PROF_REPS(c) k_sec43<real, 1><<<grid, 768, lds3, c->stream>>>(a); break;
-      case 2: PROF_REPS(c) k_sec43<real, 2><<<grid, 768, lds3, c->stream>>>(a); break;
-      case 3: PROF_REPS(c) k_sec43<real, 1, true><<<grid, 768, lds3, c->stream>>>(a); break;
-      case 4: PROF_REPS(c) k_sec43<real, 2, true><<<grid, 768, lds3, c->stream>>>(a); break;
-      default: return fail(SA_ERR_UNSUPPORTED, "k_sec43: M");
-    }
-    if (c->prof) c->prof->end(c->stream);
-    HIP_TRY(hipGetLastError());
-    return SA_OK;
-  }
-  if (c->sec4 && c->ib) {
-    const size_t lds4 = c->sec4_lds + 2 * (size_t)c->w * 2;
     switch (c->M / 256) {
-      case 1: PROF_REPS(c) k_sec4<real, 1, true><<<grid, 512, lds4, c->stream>>>(a); break;
-      case 2: PROF_REPS(c) k_sec4<real, 2, true><<<grid, 512, lds4, c->stream>>>(a); break;
-      default: return fail(SA_ERR_UNSUPPORTED, "k_sec4<IB>: M");
+      case 1: PROF_REPS(c) k_sec43<real, 1><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
+      case 2: PROF_REPS(c) k_sec43<real, 2><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
+      default: return fail(SA_ERR_UNSUPPORTED, "k_sec43: M");
     }
     if (c->prof) c->prof->end(c->stream);
     HIP_TRY(hipGetLastError());
@@ -3775,73 +3488,6 @@ int pt_for(const sa_ctx* c, int B, bool sec2) {
   return (sec2 && (c->sec3 || c->sec4) && (rk == 1 || rk == 4) && c->pt_on) ? (rk == 4 ? 16 : kRow2Rows) : 0;
 }
 
-// The fused path (row step of t-1 + hand-off + section step of t in one
-// launch) for one codeword on the pair / triple kernels with row-block-major
-// partials: every workgroup must be resident at once (one per CU at most),
-// k_row2's single-pass sums (G, Gb <= 256), the z^2 partials in the section
-// kernel's registers (<= 320) and the two row blocks' sums in the z region of LDS.
-int fused_rows(const sa_ctx* c) { return c->row16 ? 16 : kRow2Rows; }
-bool use_fused(const sa_ctx* c, int B, int pt) {
-  if (!c->fuse || B != 1 || pt == 0 || !use_sec2(c, B) || !(c->sec4 || c->sec3)) return false;
-  if (c->M != 256 && c->M != 512) return false;  // instantiated section sizes
-  const int G = sec2_parts(c), R = fused_rows(c);
-  const int NB = R == 16 ? c->NZh : c->NZ16;
-  const size_t zbytes = ((size_t)(c->n + 1) * rsz(c) + 15) / 16 * 16;
-  return pt == R && G <= 256 && G <= c->n_cus && NB <= 2 * G && NB <= 320 &&  // NB < G: some workgroups only hand off
-         2 * (512 / R) * (R + 1) * rsz(c) <= zbytes;
-}
-
-template <typename real, int FR>
-void launch_fused_r(sa_ctx* c, const SecArgs<real>& a, FuseArgs<real> f) {
-  dim3 grid(a.G, 1);
-  PROF_REPS(c) {
-    f.target = (unsigned)a.G * ++c->bar_seq;
-    bool done = false;
-    if constexpr (FR == kRow2Rows) {
-      if (c->sec3) {
-        if (c->M == 256) k_sec43f<real, 1, FR><<<grid, 768, c->sec3_lds, c->stream>>>(a, f);
-        else k_sec43f<real, 2, FR><<<grid, 768, c->sec3_lds, c->stream>>>(a, f);
-        done = true;
-      }
-    }
-    if (!done) {
-      if (c->M == 256) k_sec4f<real, 1, FR><<<grid, 512, c->sec4_lds, c->stream>>>(a, f);
-      else k_sec4f<real, 2, FR><<<grid, 512, c->sec4_lds, c->stream>>>(a, f);
-    }
-  }
-}
-
-// K_t (t >= 1): row step t-1 reads z_{t-1} from zin and publishes z_t in zout,
-// the section step t reads zout.
-template <typename real>
-int launch_fused(sa_ctx* c, int t, int es, void* bin, void* bout, void* zin, void* zout, int pt, int G, int Gb) {
-  SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
-  a.pt = pt;
-  a.beta = (real*)bin;
-  a.beta_out = (real*)bout;
-  a.G = sec2_parts(c);
-  a.z = (const real*)zout;
-  FuseArgs<real> f;
-  f.r = row_args<real>(c, ROW_AMP, t - 1, es, G, Gb);
-  f.r.pt = pt;
-  f.r.z = (real*)zout;
-  f.r.z_in = (const real*)zin;
-  f.bar = c->d_bar;
-  f.err = c->d_err;
-  f.NB = fused_rows(c) == 16 ? c->NZh : c->NZ16;
-  f.target = 0;
-  if (c->prof) c->prof->begin(c->stream, K_SEC);
-  if (fused_rows(c) == 16) {
-    if (c->sec3) return fail(SA_ERR_UNSUPPORTED, "fused triple kernel: 16-row blocks");
-    launch_fused_r<real, 16>(c, a, f);
-  } else {
-    launch_fused_r<real, kRow2Rows>(c, a, f);
-  }
-  if (c->prof) c->prof->end(c->stream);
-  HIP_TRY(hipGetLastError());
-  return SA_OK;
-}
-
 template <typename real>
 int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, void* bout = nullptr) {
   SecArgs<real> a = sec_args<real>(c, mode, t, es);
@@ -3867,11 +3513,10 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
 // The batched decode with z and the Ab partials interleaved by codeword chunk
 // (SecArgs::zil, 16-byte rows of CB codewords: binary32 CB = 4, binary64
 // CB = 2), row kernel k_rowc.  Default in binary32 (C3 +1.7 %, C4 +4.7 %);
-// binary64 only with SPARC_AMP_ZIL=1 (its k_secb spills 68 bytes against 36:
-// C3 -1.6 %, the joint decode -1.5 %); SPARC_AMP_ZIL=0 keeps [B][n] always
+// binary64 only with the plan option SA_PLAN_ZIL (its k_secb spills 68 bytes
+// against 36: C3 -1.6 %, the joint decode -1.5 %); SA_PLAN_NO_ZIL keeps [B][n]
 bool zil_for(const sa_ctx* c, int B) {
-  const char* e = getenv("SPARC_AMP_ZIL");
-  const bool on = e ? e[0] != '0' : c->prec == SA_PREC_F32;
+  const bool on = (c->plan & SA_PLAN_ZIL) ? true : (c->plan & SA_PLAN_NO_ZIL) ? false : c->prec == SA_PREC_F32;
   return on && c->backend == SA_BACKEND_HADAMARD && use_batched(c, B) && c->CB * (int)rsz(c) == 16;
 }
 
@@ -3932,31 +3577,34 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt 
   return SA_OK;
 }
 
-DenseArgs dense_args(sa_ctx* c, int t, int es, int mode) {
-  DenseArgs a;
-  a.A = c->d_A; a.z = (const float*)c->d_z; a.azp = (float*)c->d_azp;
-  a.beta = (const float*)c->d_beta; a.abp = (float*)c->d_abp; a.zzp = (const float*)c->d_zzp;
-  a.tau = (const float*)c->d_tau;
+template <typename real>
+DenseArgs<real> dense_args(sa_ctx* c, int t, int es, int mode) {
+  DenseArgs<real> a;
+  a.A = (const real*)c->d_A; a.z = (const real*)c->d_z; a.azp = (real*)c->d_azp;
+  a.beta = (const real*)c->d_beta; a.abp = (real*)c->d_abp; a.zzp = (const real*)c->d_zzp;
+  a.tau = (const real*)c->d_tau;
   a.L = c->L; a.M = c->M; a.n = c->n; a.NZ = c->nz_cur; a.T1 = c->Tcap + 1; a.t = t;
   a.early_stop = es; a.RS = c->RS; a.KS = c->KS; a.mode = mode; a.lda = c->lda;
   return a;
 }
 
+template <typename real>
 int launch_dense_az(sa_ctx* c, int B, int t, int es, int mode) {
-  DenseArgs a = dense_args(c, t, es, mode);
-  dim3 grid((unsigned)((c->lda / 4 + 255) / 256), c->RS, B);
+  DenseArgs<real> a = dense_args<real>(c, t, es, mode);
+  dim3 grid((unsigned)((c->lda / V16<real>::N + 255) / 256), c->RS, B);
   if (c->prof) c->prof->begin(c->stream, K_DAZ);
-  PROF_REPS(c) k_dense_az<<<grid, 256, 0, c->stream>>>(a);
+  PROF_REPS(c) k_dense_az<real><<<grid, 256, 0, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
 }
 
+template <typename real>
 int launch_dense_ab(sa_ctx* c, int B, int t, int es, int mode) {
-  DenseArgs a = dense_args(c, t, es, mode);
+  DenseArgs<real> a = dense_args<real>(c, t, es, mode);
   dim3 grid((unsigned)((c->n + kDenseRows - 1) / kDenseRows), c->KS, B);
   if (c->prof) c->prof->begin(c->stream, K_DAB);
-  PROF_REPS(c) k_dense_ab<<<grid, 256, 0, c->stream>>>(a, (const float*)c->d_tau);
+  PROF_REPS(c) k_dense_ab<real><<<grid, 256, 0, c->stream>>>(a, (const real*)c->d_tau);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -3977,11 +3625,11 @@ void launch_dense_den_e(sa_ctx* c, int B, const DenArgs<real>& a, bool i8) {
 // the beta digit planes written for the next A beta GEMM.  The host-operator
 // backend's A^T z is one uploaded partial as well.
 template <typename real = float>
-int launch_dense_den(sa_ctx* c, int B, int t, int es, bool i8 = false) {
+int launch_dense_den(sa_ctx* c, int B, int t, int es, bool i8 = false, bool one_partial = false) {
   DenArgs<real> a;
   a.azp = (const real*)c->d_azp; a.zzp = (const real*)c->d_zzp; a.tau = (const real*)c->d_tau;
   a.L = c->L; a.M = c->M; a.n = c->n; a.NZ = c->nz_cur; a.T1 = c->Tcap + 1; a.t = t; a.early_stop = es;
-  a.RS = (i8 || c->backend == SA_BACKEND_HOST) ? 1 : c->RS;
+  a.RS = (i8 || one_partial || c->backend == SA_BACKEND_HOST) ? 1 : c->RS;
   a.lda = c->lda;
   switch (c->E) {
     case 1: launch_dense_den_e<real, 1>(c, B, a, i8); break;
@@ -4049,6 +3697,100 @@ int i8_az(sa_ctx* c, int B, float* out, long long ldb) {
                         K_DAZ);
 }
 
+// ---- caller's dense matrix on the matrix cores (dense_mfma.hip) ----------
+bool use_fgemm(const sa_ctx* c, int B) { return c->backend == SA_BACKEND_MATRIX && B >= kFMinB; }
+
+long long f_kstage(const sa_ctx* c) { return kFKB / (long long)rsz(c); }  // K elements per stage
+
+// K splits of the A beta GEMM: the fewest (workgroup rounds x stages per
+// workgroup) on n_cus CUs at two workgroups per CU
+int fgemm_splits(const sa_ctx* c, int B) {
+  const long long tiles = (long long)(c->np / kFTY) * ((B + kFTX - 1) / kFTX);
+  const long long nst = (long long)c->lda / f_kstage(c);
+  int best = 1;
+  long long bcost = -1;
+  for (int S = 1; S <= kFMaxS; ++S) {
+    const long long rounds = (tiles * S + 2 * c->n_cus - 1) / (2 * c->n_cus);
+    const long long cost = rounds * ((nst + S - 1) / S);
+    if (bcost < 0 || cost < bcost) { bcost = cost; best = S; }
+  }
+  return best;
+}
+
+// The transposed matrix (first batched use) and the padded GEMM vectors for B codewords.
+int ensure_fgemm(sa_ctx* c, int B) {
+  if (!use_fgemm(c, B)) return SA_OK;
+  const size_t s = rsz(c);
+  int rc;
+  if (!c->d_AT) {
+    if ((rc = dev_alloc(c, &c->d_AT, (size_t)c->LMy * (size_t)c->nk * s))) return rc;
+    const dim3 grid((unsigned)((c->LMy + 63) / 64), (unsigned)((c->nk + 63) / 64));
+    if (s == 8)
+      k_transpose<double><<<grid, 256, 0, c->stream>>>((const double*)c->d_A, (long long)c->lda, c->n,
+                                                       (long long)c->L * c->M, (double*)c->d_AT, c->LMy, c->nk);
+    else
+      k_transpose<float><<<grid, 256, 0, c->stream>>>((const float*)c->d_A, (long long)c->lda, c->n,
+                                                      (long long)c->L * c->M, (float*)c->d_AT, c->LMy, c->nk);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  if (B > c->fg_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    drop_graphs(c);
+    dev_free(c->d_xz); dev_free(c->d_xb);
+    c->d_xz = c->d_xb = nullptr;
+    c->fg_cap = 0;
+    if ((rc = dev_alloc(c, &c->d_xz, (size_t)B * (size_t)c->nk * s))) return rc;
+    if ((size_t)c->L * c->M != c->lda && (rc = dev_alloc(c, &c->d_xb, (size_t)B * c->lda * s))) return rc;
+    c->fg_cap = B;
+  }
+  return SA_OK;
+}
+
+template <typename real>
+int launch_gemm_f(sa_ctx* c, int B, const real* X, long long ldx, const real* Y, long long ldy, long long K,
+                  long long Yrows, int Ny, real* out, long long ldb, long long lds, int S, int kind) {
+  FArgs<real> a;
+  a.X = X; a.Y = Y; a.out = out; a.ldx = ldx; a.ldy = ldy; a.ldb = ldb; a.lds = lds;
+  a.nst = (int)(K / f_kstage(c));
+  a.kps = (a.nst + S - 1) / S;
+  a.XT = (B + kFTX - 1) / kFTX; a.YT = (int)(Yrows / kFTY); a.S = S; a.B = B; a.Ny = Ny;
+  if (K % f_kstage(c) || Yrows % kFTY || ldx < K || ldy < K || B > c->fg_cap)
+    return fail(SA_ERR_ARG, "k_gemm_f: operand shapes");
+  const long long grid = (long long)a.XT * a.YT * S;
+  if (grid > 0x7fffffff) return fail(SA_ERR_UNSUPPORTED, "k_gemm_f: grid too large");
+  if (c->prof) c->prof->begin(c->stream, kind);
+  PROF_REPS(c) k_gemm_f<real><<<(unsigned)grid, 512, kFLds, c->stream>>>(a);
+  if (c->prof) c->prof->end(c->stream);
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
+// A beta of the beta in d_beta on the GEMM path: S partials [B][S][n] in d_abp
+template <typename real>
+int fgemm_ab(sa_ctx* c, int B, int S) {
+  const long long LM = (long long)c->L * c->M;
+  const real* X = (const real*)c->d_beta;
+  if (LM != (long long)c->lda) {  // L*M not a whole number of K stages: a zero-padded copy
+    k_pad_rows<real><<<4096, 256, 0, c->stream>>>((const real*)c->d_beta, LM, LM, (real*)c->d_xb, (long long)c->lda,
+                                                  B);
+    HIP_TRY(hipGetLastError());
+    X = (const real*)c->d_xb;
+  }
+  return launch_gemm_f<real>(c, B, X, (long long)c->lda, (const real*)c->d_A, (long long)c->lda, (long long)c->lda,
+                             c->np, c->n, (real*)c->d_abp, (long long)S * c->n, c->n, S, K_DAB);
+}
+
+// A^T z of the z in d_z on the GEMM path into out[b][0 .. L*M) (rows ldb apart)
+template <typename real>
+int fgemm_az(sa_ctx* c, int B, real* out, long long ldb) {
+  k_pad_rows<real><<<4096, 256, 0, c->stream>>>((const real*)c->d_z, (long long)c->n, (long long)c->n,
+                                                (real*)c->d_xz, c->nk, B);
+  HIP_TRY(hipGetLastError());
+  return launch_gemm_f<real>(c, B, (const real*)c->d_xz, c->nk, (const real*)c->d_AT, c->nk, c->nk, c->LMy,
+                             c->L * c->M, out, ldb, 0, 1, K_DAZ);
+}
+
 // ---- composite sequences (all asynchronous on c->stream) ----------------
 
 // Ab of the batch staged in d_beta -> d_out  (B x n)
@@ -4060,8 +3802,13 @@ int seq_ab(sa_ctx* c, int B) {
     if ((rc = i8_ab_any(c, B, S))) return rc;
     return launch_row<real>(c, B, ROW_ABOUT, 0, 0, S, c->Gd);
   }
-  if (c->backend == SA_BACKEND_DENSE) {
-    if ((rc = launch_dense_ab(c, B, 0, 0, 1))) return rc;
+  if (use_fgemm(c, B)) {
+    const int S = fgemm_splits(c, B);
+    if ((rc = fgemm_ab<real>(c, B, S))) return rc;
+    return launch_row<real>(c, B, ROW_ABOUT, 0, 0, S, c->Gd);
+  }
+  if (is_dense(c)) {
+    if ((rc = launch_dense_ab<real>(c, B, 0, 0, 1))) return rc;
     return launch_row<real>(c, B, ROW_ABOUT, 0, 0, c->KS, c->Gd);
   }
   if ((rc = launch_sec<real>(c, B, SEC_AB, 0, 0))) return rc;
@@ -4069,34 +3816,32 @@ int seq_ab(sa_ctx* c, int B) {
 }
 
 // Az of the batch staged in d_z -> d_out  (B x L*M)
-template <typename real>
-int seq_az(sa_ctx* c, int B);
 
-template <>
-int seq_az<float>(sa_ctx* c, int B) {
-  if (use_i8(c, B)) return i8_az(c, B, (float*)c->d_out, (long long)c->L * c->M);
-  if (c->backend == SA_BACKEND_DENSE) {
-    int rc = launch_dense_az(c, B, 0, 0, 1);
+template <typename real>
+int seq_az(sa_ctx* c, int B) {
+  if constexpr (sizeof(real) == 4)
+    if (use_i8(c, B)) return i8_az(c, B, (float*)c->d_out, (long long)c->L * c->M);
+  if (use_fgemm(c, B)) return fgemm_az<real>(c, B, (real*)c->d_out, (long long)c->L * c->M);
+  if (is_dense(c)) {
+    int rc = launch_dense_az<real>(c, B, 0, 0, 1);
     if (rc) return rc;
-    // reduce partials into d_out
-    // (small op: reuse k_convert-like loop via a lambda kernel is not possible;
-    //  use a dedicated reduction below)
+    // the RS row-split partials into d_out
+    k_dense_az_reduce<real><<<4096, 256, 0, c->stream>>>((const real*)c->d_azp, (real*)c->d_out, c->RS, c->lda,
+                                                         (size_t)c->L * c->M, B);
+    HIP_TRY(hipGetLastError());
     return SA_OK;
   }
-  return launch_sec<float>(c, B, SEC_AZ, 0, 0);
-}
-template <>
-int seq_az<double>(sa_ctx* c, int B) {
-  return launch_sec<double>(c, B, SEC_AZ, 0, 0);
+  return launch_sec<real>(c, B, SEC_AZ, 0, 0);
 }
 
 // Whole AMP decode of the staged batch: y in d_y, beta0 in d_beta if has_b0.
 template <typename real>
 int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   const int es = (flags & SA_FLAG_NO_EARLY_STOP) ? 0 : 1;
-  const bool dense = c->backend == SA_BACKEND_DENSE;
+  const bool dense = is_dense(c);
   const bool i8 = use_i8(c, B);
-  const int S8 = i8 ? i8_splits(c, B) : 0;
+  const bool fg = use_fgemm(c, B);
+  const int S8 = i8 ? i8_splits(c, B) : (fg ? fgemm_splits(c, B) : 0);
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
   pick_row(c, B);  // row kernel and its z^2 partial count
@@ -4104,7 +3849,7 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
   // Ab partials row-block major between the pair / triple kernels and k_row2
   const int pt = pt_for(c, B, sec2);
   // partial counts of the producer of abp (Ab) and bbp (beta^2)
-  const int G = i8 ? S8 : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
+  const int G = (i8 || fg) ? S8 : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
   const int Gb = dense ? c->Gd : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G));
   int rc;
   k_fill32<<<(B + 255) / 256, 256, 0, c->stream>>>((uint32_t*)c->d_iters, 0xffffffffu, (size_t)B);
@@ -4112,8 +3857,11 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     if (i8) {
       if ((rc = i8_ab_any(c, B, S8))) return rc;
       if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, S8, c->Gd))) return rc;
+    } else if (fg) {
+      if ((rc = fgemm_ab<real>(c, B, S8))) return rc;
+      if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, S8, c->Gd))) return rc;
     } else if (dense) {
-      if ((rc = launch_dense_ab(c, B, 0, 0, 1))) return rc;
+      if ((rc = launch_dense_ab<real>(c, B, 0, 0, 1))) return rc;
       if ((rc = launch_row<real>(c, B, ROW_INIT, 0, 0, c->KS, c->Gd))) return rc;
     } else {
       if ((rc = launch_sec<real>(c, B, SEC_AB, 0, 0))) return rc;
@@ -4124,23 +3872,7 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     k_fill32<<<(int)std::min<size_t>((nw + 255) / 256, 8192), 256, 0, c->stream>>>((uint32_t*)c->d_beta, 0u, nw);
     if ((rc = launch_row<real>(c, B, ROW_INIT0, 0, 0, G, Gb))) return rc;
   }
-  const bool fused = !dense && !batched && sec2 && use_fused(c, B, pt);
-  if (fused) {
-    // the fused path: K_0 alone, then K_t = row step t-1 + section step t,
-    // then the row step T-1 alone; z double-buffered (z_t in buffer t & 1)
-    k_fill32<<<1, 256, 0, c->stream>>>(c->d_bar, 0u, (size_t)256);
-    c->bar_seq = 0;
-    void* zb[2] = {c->d_z, c->d_z2};
-    for (int t = 0; t < T; ++t) {
-      void* pin = (t & 1) ? c->d_beta2 : c->d_beta;
-      void* pout = (t & 1) ? c->d_beta : c->d_beta2;
-      if (t == 0) rc = launch_sec2<real>(c, B, t, es, pin, pout, pt);
-      else rc = launch_fused<real>(c, t, es, pin, pout, zb[(t - 1) & 1], zb[t & 1], pt, G, Gb);
-      if (rc) return rc;
-    }
-    if (T > 0 && (rc = launch_row<real>(c, B, ROW_AMP, T - 1, es, G, Gb, pt, zb[(T - 1) & 1], zb[T & 1]))) return rc;
-  }
-  for (int t = 0; t < (fused ? 0 : T); ++t) {
+  for (int t = 0; t < T; ++t) {
     if (i8) {
       // z -> digit planes -> Az GEMM (into the dense Az buffer, one partial)
       // -> denoiser (+ beta digit planes) -> A beta GEMM (S8 partials)
@@ -4149,10 +3881,17 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
       if ((rc = launch_gemm_i8<kI8NPB>(c, B, c->d_bq, c->LMp8, c->d_A8, c->np8, c->n, (float*)c->d_abp,
                                (long long)S8 * c->n, c->n, S8, c->d_bfix + 1, 0, K_DAB)))
         return rc;
+    } else if (fg) {
+      // z -> Az GEMM (one partial) -> denoiser -> A beta GEMM (S8 partials);
+      // the GEMMs skip nothing for a stopped codeword: the row kernel keeps
+      // its residual and the denoiser its estimate
+      if ((rc = fgemm_az<real>(c, B, (real*)c->d_azp, (long long)c->lda))) return rc;
+      if ((rc = launch_dense_den<real>(c, B, t, es, false, true))) return rc;
+      if ((rc = fgemm_ab<real>(c, B, S8))) return rc;
     } else if (dense) {
-      if ((rc = launch_dense_az(c, B, t, es, 0))) return rc;
-      if ((rc = launch_dense_den(c, B, t, es))) return rc;
-      if ((rc = launch_dense_ab(c, B, t, es, 0))) return rc;
+      if ((rc = launch_dense_az<real>(c, B, t, es, 0))) return rc;
+      if ((rc = launch_dense_den<real>(c, B, t, es))) return rc;
+      if ((rc = launch_dense_ab<real>(c, B, t, es, 0))) return rc;
     } else if (batched) {
       if ((rc = launch_secb<real>(c, B, t, es))) return rc;
     } else {
@@ -4174,17 +3913,12 @@ int seq_amp(sa_ctx* c, int B, int T, int flags, int has_b0) {
     k_beta_final<real><<<dim3((unsigned)std::min<size_t>((LM + 255) / 256, 4096), B), 256, 0, c->stream>>>(
         (real*)c->d_beta, (const real*)c->d_beta2, c->d_iters, LM);
     HIP_TRY(hipGetLastError());
-    if (fused) {
-      k_z_final<real><<<(c->n + 255) / 256, 256, 0, c->stream>>>((real*)c->d_z, (const real*)c->d_z2, c->d_iters,
-                                                                  c->n);
-      HIP_TRY(hipGetLastError());
-    }
   }
   return SA_OK;
 }
 
 int ensure_beta2(sa_ctx* c, int B) {
-  if (c->backend == SA_BACKEND_DENSE || use_batched(c, B) || c->beta2_cap >= c->Bcap) return SA_OK;
+  if (is_dense(c) || use_batched(c, B) || c->beta2_cap >= c->Bcap) return SA_OK;
   HIP_TRY(hipStreamSynchronize(c->stream));
   dev_free(c->d_beta2);
   c->d_beta2 = nullptr;
@@ -4203,13 +3937,14 @@ int run_graph(sa_ctx* c, int B, int T, int flags, int has_b0) {
   int rc0 = ensure_beta2(c, B);
   if (!rc0 && use_batched(c, B)) rc0 = ensure_invb(c);  // before any capture: it uploads
   if (rc0) return rc0;
-  if (getenv("SPARC_AMP_NO_GRAPH")) {  // debug aid: eager launches instead of the captured graph
+  if (c->plan & SA_PLAN_EAGER) {  // eager launches instead of the captured graph
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     int rc = seq_amp<real>(c, B, T, flags, has_b0);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->last_B = B;
     c->last_T = T;
+    c->zil_last = zil_for(c, B);
     return SA_OK;
   }
   // the power-allocation mode selects the captured kernel arguments (c, P arrays)
@@ -4238,11 +3973,22 @@ int run_graph(sa_ctx* c, int B, int T, int flags, int has_b0) {
   HIP_TRY(hipEventRecord(c->ev1, c->stream));
   c->last_B = B;
   c->last_T = T;
+  c->zil_last = zil_for(c, B);  // the layout d_z is left in by THIS run (a cached graph does not run seq_amp)
   return SA_OK;
 }
 
 int check_ctx(const sa_ctx* c) {
   if (!c) return fail(SA_ERR_ARG, "null context");
+  return SA_OK;
+}
+
+// Entry points that read the Hadamard design's tables (the row-parallel
+// encoder and cancellation: one table entry per section and row).
+int check_tables(const sa_ctx* c, const char* what) {
+  if (!c) return fail(SA_ERR_ARG, "null context");
+  if (c->backend != SA_BACKEND_HADAMARD && c->backend != SA_BACKEND_DENSE)
+    return fail(SA_ERR_UNSUPPORTED, std::string(what) + ": needs a design built from an ordering "
+                                                        "(use sa_Ab for a caller's matrix)");
   return SA_OK;
 }
 
@@ -4287,7 +4033,7 @@ int set_power(sa_ctx* c, const double* Pl) {
 // (amp_exit.py:113-116) as a mask, per codeword, in one batch.
 int set_power_batch(sa_ctx* c, int B, const double* Pl) {
   if (!Pl) return fail(SA_ERR_ARG, "Pl is NULL");
-  if (c->backend == SA_BACKEND_DENSE) return fail(SA_ERR_UNSUPPORTED, "per-codeword power: Hadamard backend only");
+  if (is_dense(c)) return fail(SA_ERR_UNSUPPORTED, "per-codeword power: Hadamard backend only");
   const size_t L = (size_t)c->L;
   std::vector<double> cb((size_t)B * L), Pb(B);
   for (int b = 0; b < B; ++b) {
@@ -4317,9 +4063,6 @@ int build_tables(sa_ctx* c) {
   std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);  // [G][n][4]; missing sections -> (k 0, +)
   std::vector<uint32_t> fwd2((size_t)((L + 1) / 2) * n, 0);  // [L/2][n] section pairs
   std::vector<uint32_t> fwd3(c->sec3 ? (size_t)c->G3 * n : 0, 0);  // [L/3][n] section triples
-  // ordering values for the in-LDS bucket tables (c->ib): pairs o0 | o1 << 16, triples (o0 | o1 << 16, o2)
-  std::vector<uint32_t> fwo2(c->ib && !c->sec3 ? (size_t)((L + 1) / 2) * n : 0, 0);
-  std::vector<uint32_t> fwo3(c->ib && c->sec3 ? (size_t)c->G3 * n * 2 : 0, 0);
   for (int l = 0; l < L; ++l) {
     const uint32_t* o = c->ordering.data() + (size_t)l * n;
     uint16_t* il = inv.data() + (size_t)l * w;
@@ -4337,8 +4080,6 @@ int build_tables(sa_ctx* c) {
       fwd2[(size_t)(l / 2) * n + r] |= (uint32_t)e << (16 * (l & 1));
       if (c->sec3)  // M <= 512: k in 9 bits, the sign in bit 9 of a 10-bit field
         fwd3[(size_t)(l / 3) * n + r] |= (uint32_t)((e & 0x1ffu) | ((e >> 15) << 9)) << (10 * (l % 3));
-      if (!fwo2.empty()) fwo2[(size_t)(l / 2) * n + r] |= v << (16 * (l & 1));
-      if (!fwo3.empty()) fwo3[((size_t)(l / 3) * n + r) * 2 + (l % 3 == 2)] |= v << (l % 3 == 1 ? 16 : 0);
     }
   }
   int rc;
@@ -4346,8 +4087,6 @@ int build_tables(sa_ctx* c) {
   if ((rc = dev_alloc(c, (void**)&c->d_fwd, fwd.size() * 2))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_fwd2, fwd2.size() * 4))) return rc;
   if (c->sec3 && (rc = dev_alloc(c, (void**)&c->d_fwd3, fwd3.size() * 4))) return rc;
-  if (!fwo2.empty() && (rc = dev_alloc(c, (void**)&c->d_fwo2, fwo2.size() * 4))) return rc;
-  if (!fwo3.empty() && (rc = dev_alloc(c, (void**)&c->d_fwo3, fwo3.size() * 4))) return rc;
   // On the context's (non-blocking) stream and waited for: a pageable
   // hipMemcpy may return once the data is staged, before the DMA lands, and
   // the null stream does not order the kernels of a non-blocking stream.
@@ -4356,10 +4095,6 @@ int build_tables(sa_ctx* c) {
   HIP_TRY(hipMemcpyAsync(c->d_fwd2, fwd2.data(), fwd2.size() * 4, hipMemcpyHostToDevice, c->stream));
   if (c->sec3)
     HIP_TRY(hipMemcpyAsync(c->d_fwd3, fwd3.data(), fwd3.size() * 4, hipMemcpyHostToDevice, c->stream));
-  if (!fwo2.empty())
-    HIP_TRY(hipMemcpyAsync(c->d_fwo2, fwo2.data(), fwo2.size() * 4, hipMemcpyHostToDevice, c->stream));
-  if (!fwo3.empty())
-    HIP_TRY(hipMemcpyAsync(c->d_fwo3, fwo3.data(), fwo3.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
@@ -4496,17 +4231,14 @@ int build_banked(sa_ctx* c, const std::vector<int>& sets, int gsize, int nbank, 
   return SA_OK;
 }
 
-bool banks_enabled() {
-  const char* e = getenv("SPARC_AMP_BANKS");
-  return !(e && e[0] == '0');
-}
+bool banks_enabled(const sa_ctx* c) { return !(c->plan & SA_PLAN_NO_BANKS); }
 
 // k_secb (16-byte rows: binary32 CB = 4, binary64 CB = 2; E >= 4): lane L of a
 // wave holds columns elem_index<E>(L ^ 3 in binary32, i) (quad-mirrored positions)
 int ensure_invb(sa_ctx* c) {
   if (c->invb_done) return SA_OK;
   c->invb_done = true;
-  if (!(banks_enabled() && c->backend == SA_BACKEND_HADAMARD && c->CB > 0 && c->CB * (int)rsz(c) == 16 &&
+  if (!(banks_enabled(c) && c->backend == SA_BACKEND_HADAMARD && c->CB > 0 && c->CB * (int)rsz(c) == 16 &&
         c->E >= 4 && c->nhi >= 2 && c->n + kInvbZeroRows <= 65535))
     return SA_OK;
   const bool sgn = c->prec == SA_PREC_F32;  // k_secb's SGN (E >= 2)
@@ -4529,7 +4261,7 @@ int build_dense(sa_ctx* c) {
   HIP_TRY(hipMalloc(&d_ord, c->ordering.size() * 4));
   HIP_TRY(hipMemcpyAsync(d_ord, c->ordering.data(), c->ordering.size() * 4, hipMemcpyHostToDevice, c->stream));
   const float s = (float)(1.0 / std::sqrt((double)n));
-  k_dense_build<<<8192, 256, 0, c->stream>>>(d_ord, c->d_A, L, M, n, w, c->lda, s);
+  k_dense_build<<<8192, 256, 0, c->stream>>>(d_ord, (float*)c->d_A, L, M, n, w, c->lda, s);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   (void)hipFree(d_ord);
@@ -4550,7 +4282,6 @@ hipError_t lds_attr_all() {
   SA_A((k_sec4<real, 1>)) SA_A((k_sec4<real, 2>)) SA_A((k_sec4<real, 4>)) SA_A((k_sec4<real, 8>))
   SA_A((k_sec4<real, 16>))
   SA_A((k_sec43<real, 1>)) SA_A((k_sec43<real, 2>))
-  SA_A((k_sec4<real, 1, true>)) SA_A((k_sec4<real, 2, true>)) SA_A((k_sec43<real, 1, true>)) SA_A((k_sec43<real, 2, true>))
   SA_A((k_secb<real, 1, 1, kWB>)) SA_A((k_secb<real, 2, 1, kWB>)) SA_A((k_secb<real, 4, 1, kWB>))
   SA_A((k_secb<real, 8, 1, kWB>)) SA_A((k_secb<real, 16, 1, kWB>))
   SA_A((k_secb<real, 1, 2, kWB>)) SA_A((k_secb<real, 2, 2, kWB>)) SA_A((k_secb<real, 4, 2, kWB>))
@@ -4608,20 +4339,27 @@ int set_lds_limits() {
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_gemm_i8<kI8NPB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             I8Tile<kI8NPB>::Lds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_gemm_f<float>, hipFuncAttributeMaxDynamicSharedMemorySize, kFLds);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_gemm_f<double>, hipFuncAttributeMaxDynamicSharedMemorySize, kFLds);
   if (e != hipSuccess) return fail(SA_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
   done = 1;
   return SA_OK;
 }
 
 int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int backend, int prec,
-                int device) {
+                int device, int plan) {
   if (!out) return fail(SA_ERR_ARG, "out is NULL");
   *out = nullptr;
   if (L <= 0 || M <= 0 || n <= 0) return fail(SA_ERR_ARG, "L, M, n must be positive");
-  if (backend != SA_BACKEND_HADAMARD && backend != SA_BACKEND_DENSE && backend != SA_BACKEND_HOST)
+  if (backend != SA_BACKEND_HADAMARD && backend != SA_BACKEND_DENSE && backend != SA_BACKEND_HOST &&
+      backend != SA_BACKEND_MATRIX)
     return fail(SA_ERR_ARG, "unknown backend");
-  if (!ordering && backend != SA_BACKEND_HOST) return fail(SA_ERR_ARG, "ordering is NULL");
+  if (!ordering && backend != SA_BACKEND_HOST && backend != SA_BACKEND_MATRIX)
+    return fail(SA_ERR_ARG, "ordering is NULL");
   if (prec != SA_PREC_F32 && prec != SA_PREC_F64) return fail(SA_ERR_ARG, "unknown precision");
+  if (plan & ~SA_PLAN_ALL) return fail(SA_ERR_ARG, "unknown plan option bits");
   if (backend == SA_BACKEND_DENSE && prec != SA_PREC_F32)
     return fail(SA_ERR_UNSUPPORTED, "dense backend streams an fp32 matrix (precision must be F32)");
   const bool pow2 = (M & (M - 1)) == 0;
@@ -4636,7 +4374,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   HIP_TRY(hipSetDevice(device));
 
   sa_ctx* c = new sa_ctx();
-  c->L = L; c->M = M; c->n = n; c->backend = backend; c->prec = prec; c->device = device;
+  c->L = L; c->M = M; c->n = n; c->backend = backend; c->prec = prec; c->device = device; c->plan = plan;
   const int mx = (M + 1) > (n + 1) ? (M + 1) : (n + 1);
   c->w = 1 << ilog2(mx);  // 2^ceil(log2(max(M+1, n+1))), sparc_ldpc.py:52/:110
   c->nhi = c->w / M;
@@ -4668,31 +4406,23 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     }
     // k_sec4: z + 2 sections' T + one exchange image per section + reductions
     const size_t need4 = zbytes + 4 * (size_t)M * s + 32 * s;
-    const char* e4 = getenv("SPARC_AMP_SEC4");
-    if (c->G2 > 0 && M >= 256 && need4 <= 160 * 1024 && !(e4 && e4[0] == '0')) {
+    if (c->G2 > 0 && M >= 256 && need4 <= 160 * 1024) {
       c->sec4 = true;
       c->sec4_lds = need4;
     }
-    // row-block-major Ab partials for k_row2 (SPARC_AMP_PT=0: the [G][n] layout):
+    // row-block-major Ab partials for k_row2 (SA_PLAN_NO_PT: the [G][n] layout):
     // each k_row2 workgroup reads one contiguous G x 128-B block instead of G
     // lines n rows apart.  C4 single codeword 880 -> 950 cw/s (k_row2 4.1 ->
     // 3.4 us, two interleaved A/B rounds); c2 within noise
-    const char* ept = getenv("SPARC_AMP_PT");
-    c->pt_on = !(ept && ept[0] == '0');
+    c->pt_on = !(plan & SA_PLAN_NO_PT);
     // 16-row k_row2 blocks for one codeword where the z^2 partials still fit
     // the section kernels' registers (ceil(n / 16) <= 320; C2: 288 workgroups
     // instead of 144, every CU pulls partials): c2 1362-1374 -> 1396 cw/s
     // (two interleaved A/B rounds).  Binary32 only: in binary64 the 32-row
     // blocks are faster (c2 fp64 984-988 -> 990-1013 cw/s, two interleaved
-    // rounds, round 3).  SPARC_AMP_R16=0/1 forces 32-/16-row blocks
-    const char* er = getenv("SPARC_AMP_R16");
-    const bool r16 = er ? er[0] != '0' : s == 4;
+    // rounds, round 3).  SA_PLAN_NO_ROW16 / SA_PLAN_ROW16 force 32- / 16-row blocks
+    const bool r16 = (plan & SA_PLAN_ROW16) ? true : (plan & SA_PLAN_NO_ROW16) ? false : s == 4;
     c->row16 = r16 && c->pt_on && c->sec4 && c->NZh <= 320;
-  }
-  {
-    // fused row step for one codeword (SPARC_AMP_FUSE=1; see FuseArgs)
-    const char* ef = getenv("SPARC_AMP_FUSE");
-    c->fuse = ef && ef[0] == '1';
   }
 
   // batched kernel: the most codewords per workgroup (CB in {4, 2, 1}; 4 for
@@ -4715,8 +4445,9 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       return {0, 0};
     };
     const auto c8 = cb_for(kWB), c16 = cb_for(kWB16);
-    const char* ew = getenv("SPARC_AMP_WB");
-    const bool w16 = ew ? atoi(ew) == kWB16 : (c16.first > c8.first || (s == 4 && c16.first == c8.first));
+    const bool w16 = (plan & SA_PLAN_WB16) ? true
+                     : (plan & SA_PLAN_WB8) ? false
+                                            : (c16.first > c8.first || (s == 4 && c16.first == c8.first));
     c->WB = w16 && c16.first > 0 ? kWB16 : kWB;
     c->CB = c->WB == kWB16 ? c16.first : c8.first;
     c->secb_lds = c->WB == kWB16 ? c16.second : c8.second;
@@ -4735,32 +4466,17 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     // chip exactly (L = 2 x CUs, c2): a third fewer 8-byte Ab partials for
     // k_row2 outweigh the longer section step (c2 fp64 989-997 -> 1026-1027
     // cw/s, two interleaved A/B rounds, round 3; binary32 at c2: neutral, pairs
-    // kept).  SPARC_AMP_SEC3=0/1 forces it off/on
+    // kept).  SA_PLAN_NO_SEC3 / SA_PLAN_SEC3 force it off / on
     const size_t need3 = (((size_t)(n + 1) * s + 15) / 16 * 16) + 6 * (size_t)M * s + 48 * s;
-    const char* e3 = getenv("SPARC_AMP_SEC3");
     const int G3 = (L + 2) / 3;
     const bool fits = c->sec4 && backend == SA_BACKEND_HADAMARD && M <= 512 && need3 <= 160 * 1024;
     const bool over = c->G2 > c->n_cus || (s == 8 && c->G2 == c->n_cus);
-    const bool want = e3 ? e3[0] == '1' : (over && G3 <= c->n_cus);
+    const bool want = (plan & SA_PLAN_SEC3) ? true : (plan & SA_PLAN_NO_SEC3) ? false : (over && G3 <= c->n_cus);
     if (fits && want) {
       c->sec3 = true;
       c->G3 = G3;
       c->sec3_lds = need3;
     }
-  }
-  {
-    // bucket tables built in LDS (secq_body<IB>) for the pair / triple
-    // kernels: M 256 or 512 (the instantiated widths), every row in one pass
-    // of the thread's Ab-table registers (pairs n <= 4608, triples n <= 8448),
-    // ordering values in 16 bits (w <= 65536) and the tables' LDS image
-    // (SPW x w x 2 B) beside the kernel's own.  SPARC_AMP_IB=0/1 forces it off/on
-    const char* eib = getenv("SPARC_AMP_IB");
-    const bool want = eib ? eib[0] == '1' : false;
-    const int spw = c->sec3 ? 3 : 2;
-    const size_t lds = (c->sec3 ? c->sec3_lds : c->sec4_lds) + (size_t)spw * c->w * 2;
-    const bool fits = backend == SA_BACKEND_HADAMARD && (c->sec3 || c->sec4) && (M == 256 || M == 512) &&
-                      n <= (c->sec3 ? 8448 : 4608) && c->w <= 65536 && lds <= 160 * 1024;
-    c->ib = want && fits;
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -4775,6 +4491,21 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     if (!rc) rc = build_dense(c);
   } else if (backend == SA_BACKEND_HOST) {
     c->lda = (size_t)L * M;  // no operator on the device: the caller's products are uploaded
+  } else if (backend == SA_BACKEND_MATRIX) {
+    // the caller's matrix, uploaded by sa_create_matrix: rows of whole GEMM K
+    // stages (128 B), padded to whole 256-row tiles, zero padding
+    c->RS = 8;
+    c->KS = 8;
+    const long long ks = kFKB / (long long)s;
+    c->lda = (size_t)(((long long)L * M + ks - 1) / ks * ks);
+    c->np = ((long long)n + kFTY - 1) / kFTY * kFTY;
+    c->nk = ((long long)n + ks - 1) / ks * ks;
+    c->LMy = ((long long)L * M + kFTY - 1) / kFTY * kFTY;
+    rc = dev_alloc(c, &c->d_A, (size_t)c->np * c->lda * s);
+    if (!rc) {
+      hipError_t e = hipMemsetAsync(c->d_A, 0, (size_t)c->np * c->lda * s, c->stream);
+      if (e != hipSuccess) rc = fail(SA_ERR_HIP, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+    }
   } else {
     rc = build_tables(c);
   }
@@ -4794,17 +4525,6 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
 }
 
 }  // namespace
-
-// Dense Az partial reduction into d_out (B x L*M), used by sa_Az on the dense backend.
-__global__ void k_dense_az_reduce(const float* azp, float* out, int RS, size_t lda, size_t LM, int B) {
-  const size_t total = (size_t)B * LM;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const size_t b = i / LM, j = i % LM;
-    float s = 0.f;
-    for (int rs = 0; rs < RS; ++rs) s += azp[(b * RS + rs) * lda + j];
-    out[i] = s;
-  }
-}
 
 
 // ---------------------------------------------------------------------------
@@ -5041,11 +4761,49 @@ extern "C" {
 
 int sa_create(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int backend, int precision,
               int device) {
-  return create_impl(out, L, M, n, ordering, backend, precision, device);
+  return create_impl(out, L, M, n, ordering, backend, precision, device, SA_PLAN_DEFAULT);
+}
+
+int sa_create_ex(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int backend, int precision,
+                 int device, int plan) {
+  return create_impl(out, L, M, n, ordering, backend, precision, device, plan);
+}
+
+int sa_create_matrix(sa_ctx** out, int L, int M, int n, const double* A, int precision, int device) {
+  if (!out) return fail(SA_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (!A) return fail(SA_ERR_ARG, "A is NULL");
+  sa_ctx* c = nullptr;
+  int rc = create_impl(&c, L, M, n, nullptr, SA_BACKEND_MATRIX, precision, device, SA_PLAN_DEFAULT);
+  if (rc) return rc;
+  // the n x (L*M) row-major binary64 matrix in chunks of rows through the
+  // staging buffer (at most 32 M values), converted on the device
+  const long long LM = (long long)L * M;
+  const long long chunk = std::max(1LL, std::min<long long>(n, (32LL << 20) / LM));
+  rc = ensure_stage(c, (size_t)(chunk * LM));
+  for (long long r0 = 0; !rc && r0 < n; r0 += chunk) {
+    const long long rows = std::min<long long>(chunk, n - r0);
+    hipError_t e = hipMemcpyAsync(c->d_stage, A + r0 * LM, (size_t)(rows * LM) * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+      if (c->prec == SA_PREC_F64)
+        k_matrix_rows<double><<<4096, 256, 0, c->stream>>>(c->d_stage, (double*)c->d_A, rows, LM, c->lda, r0);
+      else
+        k_matrix_rows<float><<<4096, 256, 0, c->stream>>>(c->d_stage, (float*)c->d_A, rows, LM, c->lda, r0);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the staging buffer is reused
+    if (e != hipSuccess) rc = fail(SA_ERR_HIP, std::string("sa_create_matrix upload: ") + hipGetErrorString(e));
+  }
+  if (rc) {
+    sa_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return SA_OK;
 }
 
 int sa_subset(const sa_ctx* parent, const int64_t* sections, int Ls, sa_ctx** out) {
-  if (int rc0 = check_op(parent, "sa_subset")) return rc0;
+  if (int rc0 = check_tables(parent, "sa_subset")) return rc0;
   if (!sections || Ls <= 0) return fail(SA_ERR_ARG, "empty section subset");
   std::vector<uint32_t> ord((size_t)Ls * parent->n);
   for (int i = 0; i < Ls; ++i) {
@@ -5055,7 +4813,8 @@ int sa_subset(const sa_ctx* parent, const int64_t* sections, int Ls, sa_ctx** ou
     std::memcpy(ord.data() + (size_t)i * parent->n, parent->ordering.data() + (size_t)s * parent->n,
                 (size_t)parent->n * 4);
   }
-  return create_impl(out, Ls, parent->M, parent->n, ord.data(), parent->backend, parent->prec, parent->device);
+  return create_impl(out, Ls, parent->M, parent->n, ord.data(), parent->backend, parent->prec, parent->device,
+                     parent->plan);
 }
 
 void sa_destroy(sa_ctx* c) {
@@ -5069,9 +4828,8 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_fwd);
   dev_free(c->d_fwd2);
   dev_free(c->d_fwd3);
-  dev_free(c->d_fwo2);
-  dev_free(c->d_fwo3);
   dev_free(c->d_A);
+  dev_free(c->d_AT); dev_free(c->d_xz); dev_free(c->d_xb);
   dev_free(c->d_A8); dev_free(c->d_AT8); dev_free(c->d_zq); dev_free(c->d_bq);
   dev_free(c->d_zsc); dev_free(c->d_bsc0); dev_free(c->d_bfix);
   dev_free(c->d_c);
@@ -5112,10 +4870,6 @@ int sa_Az(sa_ctx* c, int B, const double* z, double* out) {
     rc = seq_az<double>(c, B);
   } else {
     rc = seq_az<float>(c, B);
-    if (!rc && c->backend == SA_BACKEND_DENSE && !use_i8(c, B)) {
-      k_dense_az_reduce<<<4096, 256, 0, c->stream>>>((const float*)c->d_azp, (float*)c->d_out, c->RS, c->lda, LM, B);
-      HIP_TRY(hipGetLastError());
-    }
   }
   if (rc) return rc;
   if ((rc = download(c, out, c->d_out, (size_t)B * LM))) return rc;
@@ -5170,14 +4924,6 @@ int sa_wait(sa_ctx* c) {
   if (check_ctx(c)) return SA_ERR_ARG;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if (c->fuse && c->d_err) {  // a fused launch whose arrival poll gave up: its results are not to be trusted
-    int err = 0;
-    HIP_TRY(hipMemcpy(&err, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (err) {
-      HIP_TRY(hipMemset(c->d_err, 0, sizeof(int)));
-      return fail(SA_ERR_HIP, "fused row step: the workgroup arrival poll timed out (results discarded)");
-    }
-  }
   return SA_OK;
 }
 
@@ -5393,7 +5139,7 @@ int sa_encode(sa_ctx* c, int B, const int32_t* idx, const double* noise) {
   if (check_ctx(c)) return SA_ERR_ARG;
   if (B <= 0 || !idx) return fail(SA_ERR_ARG, "sa_encode: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_encode: power allocation not staged");
-  if (int rc0 = check_op(c, "sa_encode")) return rc0;
+  if (int rc0 = check_tables(c, "sa_encode")) return rc0;
   if (!c->pow2) return fail(SA_ERR_UNSUPPORTED, "sa_encode: the row-parallel encoder needs M a power of two");
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
@@ -5489,7 +5235,7 @@ int sa_soft_beta0(sa_ctx* c, int B, int l0, int ns, const double* app, int flags
 }
 
 int sa_hard_cancel(sa_ctx* c, int B, int l0, int ns, const double* app, int flags, sa_ctx* dst, int32_t* idx_out) {
-  if (dst && check_op(c, "sa_hard_cancel")) return SA_ERR_UNSUPPORTED;
+  if (dst && check_tables(c, "sa_hard_cancel")) return SA_ERR_UNSUPPORTED;
   int rc = check_glue(c, B, l0, ns);
   if (rc) return rc;
   if (!app) return fail(SA_ERR_ARG, "sa_hard_cancel: app is NULL");
@@ -5532,7 +5278,7 @@ int sa_threshold(sa_ctx* c, int B, int l0, int ns, const double* app, int flags,
 
 int sa_cancel_scaled(sa_ctx* c, int B, const int32_t* idx, double scale, sa_ctx* dst) {
   if (check_ctx(c) || check_ctx(dst)) return SA_ERR_ARG;
-  if (int rc0 = check_op(c, "sa_cancel")) return rc0;
+  if (int rc0 = check_tables(c, "sa_cancel")) return rc0;
   if (!c->pow2) return fail(SA_ERR_UNSUPPORTED, "sa_cancel: needs M a power of two");
   if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_cancel: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_cancel: power allocation not staged");
@@ -5557,15 +5303,14 @@ int sa_cancel(sa_ctx* c, int B, const int32_t* idx, sa_ctx* dst) { return sa_can
 
 int sa_plan(sa_ctx* c, int B, int64_t* o) {
   if (check_ctx(c) || !o || B <= 0) return fail(SA_ERR_ARG, "sa_plan: bad arguments");
-  const bool dense = c->backend == SA_BACKEND_DENSE;
+  const bool dense = is_dense(c);
   const bool batched = !dense && use_batched(c, B);
   const bool sec2 = use_sec2(c, B);
   const bool i8 = use_i8(c, B);
-  const bool fused = !dense && !batched && sec2 && use_fused(c, B, pt_for(c, B, sec2));
-  o[0] = i8 ? 6 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? (fused ? 8 : (c->ib ? 10 : 5))
-                                                             : (c->sec4 ? (fused ? 7 : (c->ib ? 9 : 4)) : 1))
-                                                  : 0)));
-  o[1] = i8 ? i8_splits(c, B) : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G)));
+  const bool fg = use_fgemm(c, B);
+  o[0] = i8 ? 6 : (fg ? 7 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? 5 : (c->sec4 ? 4 : 1)) : 0))));
+  o[1] = i8 ? i8_splits(c, B)
+            : (fg ? fgemm_splits(c, B) : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G))));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;
   o[3] = batched ? c->CB : 1;
   o[4] = nz_for(c, row_kind_for(c, B));

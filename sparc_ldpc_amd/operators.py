@@ -20,7 +20,7 @@ from ._lib import as_f64, check, dptr
 
 __all__ = [
     "SparcOperator", "AbOp", "AzOp", "HostOperatorLoop", "make_ordering", "sub_fht", "block_sub_fht",
-    "sparc_transforms", "sparc_transforms_shorter", "default_device",
+    "sparc_transforms", "sparc_transforms_shorter", "dense_transforms", "default_device",
 ]
 
 _BACKENDS = {"hadamard": _lib.SA_BACKEND_HADAMARD, "dense": _lib.SA_BACKEND_DENSE}
@@ -89,7 +89,9 @@ def make_ordering(L: int, M: int, n: int, seed: int = 0) -> np.ndarray:
 class SparcOperator:
     """A device-resident SPARC design operator (one ``sa_ctx``)."""
 
-    def __init__(self, L, M, n, ordering, backend=None, precision=None, device=None):
+    def __init__(self, L, M, n, ordering, backend=None, precision=None, device=None, plan=None):
+        """plan: None (the built-in kernel choice rules) or sa_create_ex plan
+        options, an int or names such as ``("SEC3", "NO_ROW16")``."""
         lib = _lib.load()
         backend = backend or DEFAULT_BACKEND
         precision = precision or DEFAULT_PRECISION
@@ -104,10 +106,15 @@ class SparcOperator:
         self.backend, self.precision = backend, precision
         self.device = default_device() if device is None else int(device)
         self.ordering = ordering
+        self.plan_bits = _lib.plan_bits(plan)
         self._ctx = _lib.ct.c_void_p()
-        check(lib.sa_create(_lib.ct.byref(self._ctx), self.L, self.M, self.n,
-                            ordering.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_uint32)),
-                            _BACKENDS[backend], _PRECS[precision], self.device))
+        ordp = ordering.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_uint32))
+        if self.plan_bits:
+            check(lib.sa_create_ex(_lib.ct.byref(self._ctx), self.L, self.M, self.n, ordp,
+                                   _BACKENDS[backend], _PRECS[precision], self.device, self.plan_bits))
+        else:
+            check(lib.sa_create(_lib.ct.byref(self._ctx), self.L, self.M, self.n, ordp,
+                                _BACKENDS[backend], _PRECS[precision], self.device))
         self._lib = lib
 
     def __del__(self):
@@ -118,6 +125,30 @@ class SparcOperator:
             except Exception:
                 pass
             self._ctx = None
+
+    @classmethod
+    def from_matrix(cls, A, L, M, precision=None, device=None):
+        """A caller's own dense design (SA_BACKEND_MATRIX): A is n x (L*M);
+        Ab(β) = A β and Az(z) = Aᵀ z as given (no 1/√n), on the device in
+        `precision` (GEMVs below 4 codewords, MFMA GEMMs from 4)."""
+        lib = _lib.load()
+        precision = precision or DEFAULT_PRECISION
+        if precision not in _PRECS:
+            raise ValueError(f"precision must be one of {sorted(_PRECS)}")
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        assert A.ndim == 2 and A.shape[1] == L * M, "A must be n x (L*M)"
+        self = cls.__new__(cls)
+        self.L, self.M, self.n = int(L), int(M), int(A.shape[0])
+        self.w = None
+        self.backend, self.precision = "matrix", precision
+        self.device = default_device() if device is None else int(device)
+        self.ordering = None
+        self.plan_bits = 0
+        self._ctx = _lib.ct.c_void_p()
+        check(lib.sa_create_matrix(_lib.ct.byref(self._ctx), self.L, self.M, self.n, dptr(A), _PRECS[precision],
+                                   self.device))
+        self._lib = lib
+        return self
 
     @property
     def ctx(self):
@@ -227,9 +258,7 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, None, it.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return it
 
-    # k_sec4i / k_sec43i: the pair / triple kernels with their bucket tables built in LDS (SecArgs::ib)
-    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43", "dense_mfma", "k_sec4f", "k_sec43f",
-                       "k_sec4i", "k_sec43i")
+    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43", "dense_mfma", "matrix_mfma")
 
     def fetch_z(self, B):
         """Residual z after the last decode's final iteration, (B, n)."""
@@ -351,8 +380,10 @@ class SparcOperator:
     def subset(self, sections) -> "SparcOperator":
         """Operator over the given parent sections (sparc_transforms_shorter)."""
         sec = np.ascontiguousarray(np.asarray(sections, dtype=np.int64).reshape(-1))
+        if self.ordering is None:
+            raise ValueError("subset() needs a design built from an ordering")
         return SparcOperator(len(sec), self.M, self.n, self.ordering[sec],
-                             self.backend, self.precision, self.device)
+                             self.backend, self.precision, self.device, self.plan_bits)
 
 
 class HostOperatorLoop:
@@ -489,6 +520,17 @@ def sparc_transforms(L, M, n, seed=0, *, backend=None, precision=None, device=No
     ordering = make_ordering(L, M, n, seed)
     op = _cached_operator(L, M, n, ordering, backend, precision, device)
     return AbOp(op), AzOp(op), ordering
+
+
+def dense_transforms(A, L, M, *, precision=None, device=None):
+    """A caller's own dense n x (L*M) design (e.g. an i.i.d. Gaussian matrix)
+    as device operators: returns (Ab, Az) with Ab(β) = A β, Az(z) = Aᵀ z —
+    the callables a reference caller would write as ``lambda b: A @ b`` /
+    ``lambda z: A.T @ z`` for amp() (sparc_ldpc.py:189,213,220) — so that
+    ``amp(y, σ, Pl, L, M, T, Ab, Az)`` keeps the whole loop on the device.
+    Not cached: each call copies A to the device."""
+    op = SparcOperator.from_matrix(A, L, M, precision=precision, device=device)
+    return AbOp(op), AzOp(op)
 
 
 def sparc_transforms_shorter(L, M, n, ordering, *, backend=None, precision=None, device=None):

@@ -275,19 +275,16 @@ def test_batch_matches_single_and_deterministic(sp, prec, L, M, B):
                                              ("fp32", 1025, "k_rowc", "1"), ("fp64", 1026, "k_rowc", "1"),
                                              ("fp64", 1025, "k_rowc", "1"), ("fp32", 1024, "k_rowc", None),
                                              ("fp64", 1026, "k_rowv16B", None)])
-def test_row_kernel_variants_vs_oracle(sp, prec, n, want, zil, monkeypatch):
+def test_row_kernel_variants_vs_oracle(sp, prec, n, want, zil):
     """Every batched row kernel (the Onsager residual of sparc_ldpc.py:220 and
     the A beta sum of :143-146): with z and the Ab partials codeword-interleaved
-    (k_rowc: the binary32 default, binary64 with SPARC_AMP_ZIL=1) and, with
-    SPARC_AMP_ZIL=0 (the binary64 default), k_rowv with 16-byte rows (binary32 n % 4 == 0, binary64 n
+    (k_rowc: the binary32 default, binary64 with plan option ZIL) and, with
+    NO_ZIL (the binary64 default), k_rowv with 16-byte rows (binary32 n % 4 == 0, binary64 n
     even), with 8-byte rows (binary32 n even), k_row for odd n; each chosen at
     B = 128 and checked against the oracle codeword by codeword."""
     L, M, B, P, T = 128, 256, 128, 2.0, 4
-    if zil is None:
-        monkeypatch.delenv("SPARC_AMP_ZIL", raising=False)
-    else:
-        monkeypatch.setenv("SPARC_AMP_ZIL", zil)
-    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=prec)
+    plan = None if zil is None else ("ZIL" if zil == "1" else "NO_ZIL")
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=prec, plan=plan)
     assert op.plan(B)["row_kernel"] == want, op.plan(B)
     Pl = P / L * np.ones(L)
     Ab, Az, _ = orc.sparc_transforms(L, M, n)
@@ -396,7 +393,7 @@ def test_maximum_sizes_vs_oracle(sp, prec, L, M, n):
 
 @pytest.mark.parametrize("prec", ["fp32", "fp64"])
 @pytest.mark.parametrize("L,M,n", [(258, 512, 2580), (257, 256, 2284), (300, 512, 6000)])
-def test_triple_section_kernel(sp, prec, L, M, n, monkeypatch):
+def test_triple_section_kernel(sp, prec, L, M, n):
     """k_sec43 (three sections per workgroup, chosen by default for L = 768 on
     256 CUs) forced on, incl. a missing third section (L % 3 != 0) and n past
     one row pass (n > 4608): against the oracle per iteration and against the
@@ -406,9 +403,7 @@ def test_triple_section_kernel(sp, prec, L, M, n, monkeypatch):
     ys = [orc.rep_inputs(L, M, n, Pl, 0.9, oAb, 300 + i)[1].reshape(-1) for i in range(2)]
     ops = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("SPARC_AMP_SEC3", flag)
-        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
-    monkeypatch.delenv("SPARC_AMP_SEC3")
+        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec, plan="SEC3" if flag == "1" else "NO_SEC3")
     assert ops["1"].plan(1)["section_kernel"] == "k_sec43"
     assert ops["1"].plan(1)["partials"] == (L + 2) // 3
     assert ops["0"].plan(1)["section_kernel"] == "k_sec4"
@@ -427,26 +422,23 @@ def test_triple_section_kernel(sp, prec, L, M, n, monkeypatch):
 
 @pytest.mark.parametrize("prec", ["fp32", "fp64"])
 @pytest.mark.parametrize("L,M,n,sec3", [(512, 512, 4608, "0"), (300, 512, 6007, "1"), (258, 256, 2581, "0")])
-def test_partial_layouts_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
+def test_partial_layouts_bit_identical(sp, prec, L, M, n, sec3):
     """The row-block-major Ab partials between k_sec4 / k_sec43 and k_row2
-    (the default) and the [G][n] layout (SPARC_AMP_PT=0) hold the same sums in
+    (the default) and the [G][n] layout (plan option NO_PT) hold the same sums in
     the same order: decodes bit-identical, incl. n not a multiple of the
     32-row block; and against the oracle.  The default 16-row k_row2 blocks
     (ceil(n / 16) <= 320; 32 partial groups instead of 16) against the oracle."""
     oAb, oAz, oord = orc.sparc_transforms(L, M, n)
     Pl = 2.0 / L * np.ones(L)
     y = orc.rep_inputs(L, M, n, Pl, 0.9, oAb, 77)[1].reshape(-1)
-    monkeypatch.setenv("SPARC_AMP_SEC3", sec3)
-    monkeypatch.setenv("SPARC_AMP_R16", "0")  # 32-row blocks in both layouts: the same sums
+    s3 = "SEC3" if sec3 == "1" else "NO_SEC3"
     ops = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SPARC_AMP_PT", flag)
-        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
-    monkeypatch.delenv("SPARC_AMP_PT")
-    monkeypatch.setenv("SPARC_AMP_R16", "1")  # 16-row blocks where they fit (the binary32 default)
-    ops["16"] = sp.SparcOperator(L, M, n, oord, precision=prec)
-    monkeypatch.delenv("SPARC_AMP_R16")
-    dflt = sp.SparcOperator(L, M, n, oord, precision=prec)
+    for flag in ("1", "0"):  # 32-row blocks in both layouts: the same sums
+        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec,
+                                     plan=(s3, "NO_ROW16") if flag == "1" else (s3, "NO_ROW16", "NO_PT"))
+    # 16-row blocks where they fit (the binary32 default)
+    ops["16"] = sp.SparcOperator(L, M, n, oord, precision=prec, plan=(s3, "ROW16"))
+    dflt = sp.SparcOperator(L, M, n, oord, precision=prec, plan=s3)
     assert ops["1"].plan(1)["section_kernel"] == ("k_sec43" if sec3 == "1" else "k_sec4")
     assert ops["1"].plan(1)["row_kernel"] == "k_row2"
     fits16 = (n + 15) // 16 <= 320
@@ -463,42 +455,6 @@ def test_partial_layouts_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
         b16b, _ = ops["16"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
         assert np.array_equal(b16, b16b), t  # bitwise reproducible
         assert rel(b16[0], ref) <= TOL[prec], t
-
-
-@pytest.mark.parametrize("prec", ["fp32", "fp64"])
-@pytest.mark.parametrize("L,M,n,sec3", [(512, 512, 4608, "0"), (257, 256, 2284, "0"), (258, 512, 2580, "1"),
-                                        (300, 512, 6000, "1"), (768, 512, 8294, "1")])
-def test_lds_bucket_tables_bit_identical(sp, prec, L, M, n, sec3, monkeypatch):
-    """Bucket tables built in LDS from the ordering values (SPARC_AMP_IB=1:
-    k_sec4i / k_sec43i) hold the same entries as the bucket table in HBM and
-    are gathered in the same order: decodes bit-identical to the HBM-table
-    kernels (incl. a missing second / third section and n past one row pass
-    of the pair kernel), with and without the early stop; and against the
-    oracle."""
-    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
-    Pl = 2.0 / L * np.ones(L)
-    y = orc.rep_inputs(L, M, n, Pl, 0.9, oAb, 91)[1].reshape(-1)
-    monkeypatch.setenv("SPARC_AMP_SEC3", sec3)
-    ops = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SPARC_AMP_IB", flag)
-        ops[flag] = sp.SparcOperator(L, M, n, oord, precision=prec)
-    monkeypatch.delenv("SPARC_AMP_IB")
-    base = "k_sec43" if sec3 == "1" else "k_sec4"
-    fits = (M == 256 or M == 512) and n <= (8448 if sec3 == "1" else 4608)
-    if prec == "fp64" and sec3 == "1" and n > 6000:
-        fits = False  # binary64 z (66 KB) + three 32 KB tables exceed the LDS
-    assert ops["0"].plan(1)["section_kernel"] == base
-    assert ops["1"].plan(1)["section_kernel"] == (base + "i" if fits else base)
-    for t in (1, 3):
-        b1, i1 = ops["1"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
-        b0, i0 = ops["0"].amp_batch(y.reshape(1, -1), Pl, t, early_stop=False)
-        assert np.array_equal(b1, b0) and np.array_equal(i1, i0), t
-        ref, _ = orc.amp_test(y, 0, Pl, L, M, t, oAb, oAz)
-        assert rel(b1[0], ref) <= TOL[prec], t
-    b1, i1 = ops["1"].amp_batch(y.reshape(1, -1), Pl, 25)
-    b0, i0 = ops["0"].amp_batch(y.reshape(1, -1), Pl, 25)
-    assert np.array_equal(b1, b0) and np.array_equal(i1, i0)
 
 
 def test_c4_single_uses_triples(sp):
@@ -730,3 +686,49 @@ def test_cached_operator_two_powers(sp, prec):
         if P in outs:
             assert np.array_equal(b, outs[P])
         outs[P] = b
+
+
+def test_row16_general_loop_for_kernel_partials(sp):
+    """k_row2 in 16-row blocks after a one-codeword decode must still read the
+    [G][n] partials of k_sec (sa_Ab; the beta0 start) through its general
+    loop: at ceil(L / 4) = 256 partials (L = 1024) its constant-stride fast
+    path, which assumes row-block-major partials, used to be taken (ADVICE r03
+    high).  Ab(beta) and a beta0 decode against the oracle."""
+    L, M, n, P = 1024, 256, 4096, 4.0
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp32")
+    assert op.plan(1)["row_kernel"] == "k_row2_16"
+    oAb, oAz, _ = orc.sparc_transforms(L, M, n)
+    Pl = P / L * np.ones(L)
+    _, y = orc.rep_inputs(L, M, n, Pl, 0.8, oAb, 41)
+    b1, _ = op.amp_batch(y.reshape(1, -1), Pl, 3, early_stop=False)  # leaves row_kind = 16-row k_row2
+    ref3 = orc._amp_core(y.reshape(-1, 1), Pl, L, M, 3, oAb, oAz, None, early_stop=False)[0]
+    assert rel(b1[0], ref3) <= TOL["fp32"]
+    rs = np.random.RandomState(3)
+    x = rs.randn(L * M)
+    assert rel(op.Ab_batch(x.reshape(1, -1))[0], oAb(x.reshape(-1, 1))) <= TOL["fp32"]
+    b0 = b1[0].reshape(-1, 1)
+    bb, _ = op.amp_batch(y.reshape(1, -1), Pl, 2, beta0=b0.reshape(1, -1), early_stop=False)
+    ref = orc._amp_core(y.reshape(-1, 1), Pl, L, M, 2, oAb, oAz, b0, early_stop=False)[0]
+    assert rel(bb[0], ref) <= TOL["fp32"]
+
+
+def test_fetch_z_layout_follows_every_run(sp):
+    """sa_fetch_z after a batched decode (z codeword-interleaved), a
+    one-codeword decode, and the same batched decode again from its cached
+    graph: the layout flag follows every run, not only graph captures (ADVICE
+    r03 medium), so both batched fetches agree bit for bit, and with the
+    one-codeword residual."""
+    L, M, n, B, P, T = 128, 256, 1024, 8, 2.0, 5
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp32")
+    assert op.plan(B)["row_kernel"] == "k_rowc"
+    oAb, _, _ = orc.sparc_transforms(L, M, n)
+    Pl = P / L * np.ones(L)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.6, oAb, 500 + i)[1].reshape(-1) for i in range(B)])
+    op.amp_batch(ys, Pl, T, early_stop=False)
+    za = op.fetch_z(B)
+    op.amp_batch(ys[:1], Pl, T, early_stop=False)
+    z1 = op.fetch_z(1)
+    op.amp_batch(ys, Pl, T, early_stop=False)  # replays the cached B = 8 graph
+    zb = op.fetch_z(B)
+    assert np.array_equal(za, zb)
+    assert rel(zb[0], z1[0]) <= 1e-4

@@ -105,17 +105,38 @@ def test_c1_reps(sp, prec):
         assert rel(b, g[f"beta_{r}"]) <= TOL[prec]
 
 
+def check_f64(b, g, key, NS, M, k=None):
+    """A binary64 estimate against the reference's binary64 fixture (c2_f64 /
+    c4_f64.npz): its first NS sections and the norm of the whole vector, both
+    at TOL["fp64"] = 1e-11."""
+    sfx = "" if k is None else f"_{k}"
+    b = np.asarray(b).reshape(-1)
+    assert rel(b[:NS * M], g[f"{key}{sfx}"]) <= TOL["fp64"], key
+    assert abs(np.linalg.norm(b) / float(g[f"{key}_norm{sfx}"]) - 1) <= TOL["fp64"], key
+
+
 @pytest.mark.parametrize("prec", ["fp32", "fp64"])
 def test_c2_golden(sp, prec):
-    """L=M=512 R=1 P=4, snr 10 dB (amp_test.py:161-176), T=64."""
+    """L=M=512 R=1 P=4, snr 10 dB (amp_test.py:161-176), T=64.  binary32
+    against the binary32 fixture at 1e-5; binary64 against the reference's
+    binary64 beta (c2_f64.npz) at 1e-11, at t = 1, t = 8 and the stop."""
     g = golden("c2.npz")
     L, M, n, T = int(g["L"]), int(g["M"]), int(g["n"]), int(g["T"])
     Ab, Az, _ = sp.sparc_transforms(L, M, n, precision=prec)
     Pl = float(g["P"]) / L * np.ones(L)
     y = g["y"]
-    assert rel(sp.amp(y, 0, Pl, L, M, 1, Ab, Az), g["beta_t1"]) <= max(TOL[prec], 1e-7)
+    b1 = sp.amp(y, 0, Pl, L, M, 1, Ab, Az)
     b, t = sp.amp_test(y, 0, Pl, L, M, T, Ab, Az, precision="operator")
-    assert rel(b, g["beta_final"]) <= max(TOL[prec], 1e-7)
+    if prec == "fp32":
+        assert rel(b1, g["beta_t1"]) <= TOL[prec]
+        assert rel(b, g["beta_final"]) <= TOL[prec]
+    else:
+        g64 = golden("c2_f64.npz")
+        NS = int(g64["NS"])
+        assert np.array_equal(g64["y"], y)
+        check_f64(b1, g64, "beta_t1", NS, M)
+        check_f64(sp.amp(y, 0, Pl, L, M, 8, Ab, Az, early_stop=False), g64, "beta_t8", NS, M)
+        check_f64(b, g64, "beta_final", NS, M)
     assert np.array_equal(orc.section_argmax(b, L, M), g["argmax_final"])
     # hard and soft initialisation of amp_test.py:202-240
     Lz = int(g["Lz"])
@@ -142,26 +163,37 @@ def test_c4_golden(sp, prec):
     L, M, n, T, NS = (int(g[k]) for k in ("L", "M", "n", "T", "NS"))
     Ab, Az, _ = sp.sparc_transforms(L, M, n, precision=prec)
     Pl = float(g["P"]) / L * np.ones(L)
+    g64 = golden("c4_f64.npz") if prec == "fp64" else None
     for k in (0, 1):
         y = g[f"y_{k}"]
         b1 = sp.amp(y, 0, Pl, L, M, 1, Ab, Az)
-        assert rel(b1[:NS * M], g[f"beta_t1_{k}"]) <= max(TOL[prec], 1e-7)
-        assert abs(np.linalg.norm(b1) / float(g[f"beta_t1_norm_{k}"]) - 1) <= max(TOL[prec], 1e-7)
+        if g64 is not None:
+            check_f64(b1, g64, "beta_t1", NS, M, k)
+            check_f64(sp.amp(y, 0, Pl, L, M, 8, Ab, Az, early_stop=False), g64, "beta_t8", NS, M, k)
+        else:
+            assert rel(b1[:NS * M], g[f"beta_t1_{k}"]) <= TOL[prec]
+            assert abs(np.linalg.norm(b1) / float(g[f"beta_t1_norm_{k}"]) - 1) <= TOL[prec]
         # the stop index in the operator's precision (bounds: see
         # test_stop_index_vs_reference; measured 38 / 7 in fp32, 63 / 9 in fp64
         # against the reference's 63 / 11) and the estimate it stops at
         b, t = sp.amp_test(y, 0, Pl, L, M, T, Ab, Az, precision="operator")
         t_ref = int(g[f"t_stop_{k}"])
         assert t_ref - (STOP32_EARLY if prec == "fp32" else STOP64) <= t <= t_ref + STOP64, (k, t, t_ref)
-        assert rel(b[:NS * M], g[f"beta_final_{k}"]) <= max(TOL[prec], 1e-7)
-        assert abs(np.linalg.norm(b) / float(g[f"beta_final_norm_{k}"]) - 1) <= max(TOL[prec], 1e-7)
+        if g64 is not None:
+            check_f64(b, g64, "beta_final", NS, M, k)
+        else:
+            assert rel(b[:NS * M], g[f"beta_final_{k}"]) <= TOL[prec]
+            assert abs(np.linalg.norm(b) / float(g[f"beta_final_norm_{k}"]) - 1) <= TOL[prec]
         assert np.array_equal(orc.section_argmax(b, L, M), g[f"argmax_final_{k}"])
     # the same two codewords in one batch of 8 (the batched section kernel)
     Y = np.stack([g["y_0"].reshape(-1), g["y_1"].reshape(-1)] * 4)
     bb, it = sp.amp_batch(Y, Pl, T, Ab, Az)
     for i in range(8):
         k = i % 2
-        assert rel(bb[i, :NS * M], g[f"beta_final_{k}"]) <= max(TOL[prec], 1e-7)
+        if g64 is not None:
+            check_f64(bb[i], g64, "beta_final", NS, M, k)
+        else:
+            assert rel(bb[i, :NS * M], g[f"beta_final_{k}"]) <= TOL[prec]
         assert np.array_equal(orc.section_argmax(bb[i], L, M), g[f"argmax_final_{k}"])
 
 
@@ -309,11 +341,18 @@ def test_c2_batched_golden(sp, prec):
     rs = np.random.RandomState(9)
     ys = np.stack([g["y"].reshape(-1)] + [g["y"].reshape(-1) + 0.1 * rs.randn(n) for _ in range(5)])
     bb, it = op.amp_batch(ys, Pl, T)
-    assert rel(bb[0], g["beta_final"]) <= max(TOL[prec], 1e-7)
     assert np.array_equal(orc.section_argmax(bb[0], L, M), g["argmax_final"])
-    b1, _ = op.amp_batch(ys[:1], Pl, 1)
     bt1, _ = op.amp_batch(ys, Pl, 1)
-    assert rel(bt1[0], g["beta_t1"]) <= max(TOL[prec], 1e-7)
+    if prec == "fp64":
+        g64 = golden("c2_f64.npz")
+        NS = int(g64["NS"])
+        check_f64(bb[0], g64, "beta_final", NS, M)
+        check_f64(bt1[0], g64, "beta_t1", NS, M)
+        bt8, _ = op.amp_batch(ys, Pl, 8, early_stop=False)
+        check_f64(bt8[0], g64, "beta_t8", NS, M)
+    else:
+        assert rel(bb[0], g["beta_final"]) <= TOL[prec]
+        assert rel(bt1[0], g["beta_t1"]) <= TOL[prec]
 
 
 def test_dense_backend_matches_hadamard(sp):
@@ -567,7 +606,7 @@ def test_c2_batch256_golden(sp):
         else:
             Y[s] += op.Ab_batch(b0[None, :])[0]
     b1, _ = op.amp_batch(Y, Pl, 1)
-    assert rel(b1[0], g["beta_t1"]) <= max(TOL["fp32"], 1e-7)
+    assert rel(b1[0], g["beta_t1"]) <= TOL["fp32"]
     bf, it = op.amp_batch(Y, Pl, T)
     assert rel(bf[0], g["beta_final"]) <= TOL["fp32"]
     assert np.array_equal(orc.section_argmax(bf[0], L, M), g["argmax_final"])

@@ -29,6 +29,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 I8_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF bf16 rate per clock (MI355X_MICROARCH.md, Matrix cores)
+F32_PEAK_TFLOPS = 157.3  # f32-input MFMA (v_mfma_f32_32x32x2_f32) = the f32 vector peak (MI355X_MICROARCH.md)
+F64_PEAK_TFLOPS = 78.6   # f64 MFMA (v_mfma_f64_16x16x4_f64): half the f32 rate
 NP_Z, NP_B = 3, 4      # int8 digit planes of z and beta on the dense GEMM path (csrc/dense_i8.hip)
 PROFILE_REP = 16       # back-to-back launches per event pair (roofline timing)
 
@@ -77,9 +79,9 @@ def row_bytes(n, B, G, s):
     return B * (G * n * s + 3 * n * s)
 
 
-def gemv_bytes(L, M, n):
-    """4·n·L·M + 4·(n + L·M) per fp32 GEMV."""
-    return 4 * n * L * M + 4 * (n + L * M)
+def gemv_bytes(L, M, n, s=4):
+    """4·n·L·M + 4·(n + L·M) per fp32 GEMV (s = 8: binary64)."""
+    return s * n * L * M + s * (n + L * M)
 
 
 def i8_gemm_ops(L, M, n, B, planes):
@@ -186,24 +188,36 @@ def cpu_baseline(w, procs=None, Tsample=None):
 
 
 def dense_gemv_probe(device):
-    """North-star GEMV at L=768 M=512 R=5/6 (n=8294) on the dense backend:
-    fp32 A (13.05 GB) streamed once per product; per-kernel event timing."""
+    """North-star GEMVs at L=768 M=512 R=5/6 (n=8294), one codeword, on a
+    materialised fp32 A (13.05 GB) streamed once per product: the Hadamard
+    design's matrix (dense backend) and an i.i.d. Gaussian design generated on
+    the device (matrix backend, sa_create_matrix_random; the north star's
+    "Gaussian design-matrix GEMVs"); per-kernel event timing."""
     import sparc_ldpc_amd as sp
     L, M, R, P = 768, 512, 5 / 6, 1.8
     n = int(L * np.log2(M) / R)
-    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="dense", precision="fp32", device=device)
     Pl = P / L * np.ones(L)
-    y = synth_y(op, Pl, 0.6, [7])
-    op.reserve(1, 4)
-    op.stage(y, Pl)
-    op.profile(1, 2, early_stop=False)  # warm
-    kinds, _ = op.profile(1, 2, early_stop=False, rep=4)
     gb = gemv_bytes(L, M, n) / 1e9
     out = {"workload": "L=768 M=512 R=5/6 single codeword, dense fp32 A", "bytes_per_gemv": gemv_bytes(L, M, n)}
-    for k in ("k_dense_az", "k_dense_ab"):
-        ms = kinds[k][0]
-        out[k] = {"ms": ms, "achieved_GBs": gb / (ms * 1e-3), "frac": gb / (ms * 1e-3) / HBM_PEAK_GBS}
-    del op
+    for tag, mk in (("hadamard_A", lambda: sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="dense",
+                                                               precision="fp32", device=device)),
+                    ("gaussian_A", lambda: sp.SparcOperator.from_random(L, M, n, seed=1, precision="fp32",
+                                                                        device=device))):
+        op = mk()
+        y = synth_y(op, Pl, 0.6, [7])
+        op.reserve(1, 4)
+        op.stage(y, Pl)
+        op.profile(1, 2, early_stop=False)  # warm
+        kinds, _ = op.profile(1, 2, early_stop=False, rep=4)
+        res = {}
+        for k in ("k_dense_az", "k_dense_ab"):
+            ms = kinds[k][0]
+            res[k] = {"ms": round(ms, 4), "achieved_GBs": round(gb / (ms * 1e-3), 1),
+                      "frac": round(gb / (ms * 1e-3) / HBM_PEAK_GBS, 4)}
+        out[tag] = res
+        del op
+    # the round-3 keys: the Hadamard design's GEMVs
+    out.update(out["hadamard_A"])
     return out
 
 
@@ -302,34 +316,45 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
     kinds_rep, _ = op.profile(B, min(T, 4), early_stop=False, rep=PROFILE_REP)
     s = 8 if precision == "fp64" else 4
     plan = op.plan(B)
-    mfma = plan["section_kernel"] == "dense_mfma"
+    mfma = plan["section_kernel"] in ("dense_mfma", "matrix_mfma")
+    fmfma = plan["section_kernel"] == "matrix_mfma"
     if op.backend == "hadamard":
         G = plan["partials"]
         per = {"k_sec": sec_bytes(L, M, n, op.w, B, G, s, plan["section_kernel"]), "k_row": row_bytes(n, B, G, s)}
+    elif fmfma:  # f32 / f64 MFMA GEMMs of a caller's matrix: 2 n L M B flops per product
+        per = {"k_dense_az": 2 * n * L * M * B, "k_dense_ab": 2 * n * L * M * B}
     elif mfma:
         per = {"k_dense_az": i8_gemm_ops(L, M, n, B, NP_Z), "k_dense_ab": i8_gemm_ops(L, M, n, B, NP_B)}
     else:
-        per = {"k_dense_az": gemv_bytes(L, M, n) * B, "k_dense_ab": gemv_bytes(L, M, n) * B,
-               "k_dense_den": B * (8 * 4 * L * M + 8 * L * M), "k_row": row_bytes(n, B, 8, s)}
+        per = {"k_dense_az": gemv_bytes(L, M, n, s) * B, "k_dense_ab": gemv_bytes(L, M, n, s) * B,
+               "k_dense_den": B * (8 * s * L * M + 2 * s * L * M), "k_row": row_bytes(n, B, 8, s)}
     share = {k: kinds[k][0] * kinds[k][1] for k in per}
     dom = max(share, key=share.get)
     dom_ms = kinds_rep[dom][0]
     scale = 1e12 if mfma else 1e9
-    peak = I8_PEAK_TOPS if mfma else HBM_PEAK_GBS
+    peak = (F64_PEAK_TFLOPS if precision == "fp64" else F32_PEAK_TFLOPS) if fmfma else (
+        I8_PEAK_TOPS if mfma else HBM_PEAK_GBS)
     achieved = per[dom] / (dom_ms * 1e-3) / scale
     kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom)
-    trace_name = {"k_dense_az": "k_gemm_i8_Az", "k_dense_ab": "k_gemm_i8_Ab"}[dom] if mfma else kname
-    if mfma:
+    if fmfma:
+        trace_name = {"k_dense_az": "k_gemm_f_Az", "k_dense_ab": "k_gemm_f_Ab"}[dom]
+        kname = f"k_gemm_f<{'double' if precision == 'fp64' else 'float'}> (" + {
+            "k_dense_az": "A^T z", "k_dense_ab": "A beta"}[dom] + ")"
+    elif mfma:
+        trace_name = {"k_dense_az": "k_gemm_i8_Az", "k_dense_ab": "k_gemm_i8_Ab"}[dom]
         kname = "k_gemm_i8 (" + {"k_dense_az": f"A^T z, {NP_Z} digit planes",
                                  "k_dense_ab": f"A beta, {NP_B} digit planes"}[dom] + ")"
+    else:
+        trace_name = kname
     src = source_hash()
     # consistency: the loop kernels' back-to-back times per iteration, T times
     per_iter = sum(kinds_rep[k][0] * round(kinds[k][1] / T) for k in kinds if kinds[k][1] >= T)
     roof = {
         "bound": "mfma" if mfma else "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": peak,
         "unit": "TFLOP/s" if mfma else "GB/s", "frac": round(achieved / peak, 4), "traffic": None,
-        ("algorithmic_int8_ops_per_launch" if mfma else "algorithmic_bytes_per_launch"): per[dom],
-        **({"ops": "int8 multiply-adds x 2 (TOP/s)"} if mfma else {}),
+        (("algorithmic_flops_per_launch" if fmfma else "algorithmic_int8_ops_per_launch") if mfma
+         else "algorithmic_bytes_per_launch"): per[dom],
+        **({"ops": ("multiply-adds x 2 (TFLOP/s)" if fmfma else "int8 multiply-adds x 2 (TOP/s)")} if mfma else {}),
         "avg_launch_ms": round(dom_ms, 5),
         "timing": f"HIP events on the library stream around {PROFILE_REP} back-to-back launches of each kernel "
                   f"(kernel + same-stream boundary), measured live in this run",
@@ -389,9 +414,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--backend", default="hadamard", choices=["hadamard", "dense"])
+    ap.add_argument("--backend", default="hadamard", choices=["hadamard", "dense", "matrix"],
+                    help="matrix: an i.i.d. Gaussian N(0, 1/n) design generated on the device")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
     ap.add_argument("--batch", type=int, default=0, help="override codewords per step")
+    ap.add_argument("--plan", default="", help="comma-separated plan options (sa_create_ex), e.g. ONE_PASS")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0)
@@ -423,8 +450,13 @@ def main():
     L, M, P, T, B, sigma = w["L"], w["M"], w["P"], w["T"], w["B"], w["sigma"]
     n = n_of(w)
     Pl = P / L * np.ones(L)
-    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend=args.backend,
-                          precision=args.precision, device=device)
+    if args.backend == "matrix":
+        op = sp.SparcOperator.from_random(L, M, n, seed=0, precision=args.precision, device=device)
+        w["desc"] += "; i.i.d. Gaussian N(0, 1/n) design (device-generated), not the Hadamard operator"
+    else:
+        op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend=args.backend,
+                              precision=args.precision, device=device,
+                              plan=[p for p in args.plan.split(",") if p] or None)
     # per-rank synthetic reps: seeds 1000 + rank*B + i (sharded, no overlap)
     seeds = [1000 + rank * B + i for i in range(B)]
     y = synth_y(op, Pl, sigma, seeds)
@@ -451,7 +483,8 @@ def main():
         "data": "synthetic (RandomState(seed) section indices + N(0, sigma^2) noise, y = A beta0 + w)",
         "config": {"workload": w["desc"], "L": L, "M": M, "n": n, "P": P, "sigma": round(sigma, 6), "T": T,
                    "codewords_per_step_per_gpu": B, "backend": args.backend, "precision": args.precision,
-                   "early_stop": False, "parallelism": f"reps sharded over {world} GPU(s)"},
+                   "early_stop": False, "parallelism": f"reps sharded over {world} GPU(s)",
+                   **({"plan": args.plan} if args.plan else {})},
         "roofline": roofline,
     }
     if world > 1:

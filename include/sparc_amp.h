@@ -72,8 +72,8 @@ int sa_create(sa_ctx** out, int L, int M, int n, const uint32_t* ordering,
  * normally chosen by built-in rules from (L, M, n, precision, batch, CUs)
  * (sa_plan reports the choice); these bits override a rule, e.g. to test a
  * kernel on shapes where the rule would not pick it.  Every option keeps the
- * results within the same parity bounds; SA_PLAN_NO_PT and SA_PLAN_EAGER are
- * bit-identical to the default plan.  `sa_subset` contexts
+ * results within the same parity bounds; SA_PLAN_NO_PT, SA_PLAN_EAGER and
+ * SA_PLAN_ONE_PASS are bit-identical to the default plan.  `sa_subset` contexts
  * inherit their parent's options. */
 enum {
   SA_PLAN_DEFAULT = 0,
@@ -88,7 +88,8 @@ enum {
   SA_PLAN_WB16 = 1 << 8,      /* batched: 16 sections per workgroup */
   SA_PLAN_NO_BANKS = 1 << 9,  /* batched: bucket slots summed in h order (no bank-aware slot order) */
   SA_PLAN_EAGER = 1 << 10,    /* sa_run launches eagerly instead of replaying a captured hipGraph */
-  SA_PLAN_ALL = (1 << 11) - 1
+  SA_PLAN_ONE_PASS = 1 << 11, /* batched: every section group of an XCD in one pass of the work order */
+  SA_PLAN_ALL = (1 << 12) - 1
 };
 int sa_create_ex(sa_ctx** out, int L, int M, int n, const uint32_t* ordering,
                  int backend, int precision, int device, int plan);
@@ -103,6 +104,14 @@ int sa_create_ex(sa_ctx** out, int L, int M, int n, const uint32_t* ordering,
  * (SA_ERR_UNSUPPORTED here). */
 int sa_create_matrix(sa_ctx** out, int L, int M, int n, const double* A,
                      int precision, int device);
+
+/* The same backend with an i.i.d. N(0, scale^2) design generated on the
+ * device (e.g. scale = 1/sqrt(n): unit-norm columns on average) for
+ * simulations that never need the matrix on the host: Philox4x32-10 keyed by
+ * `seed`, counter = row-major element index / 4, Box-Muller; reproducible per
+ * (seed, element), not NumPy's stream. */
+int sa_create_matrix_random(sa_ctx** out, int L, int M, int n, uint64_t seed, double scale,
+                            int precision, int device);
 
 /* Replaces sparc_transforms_shorter(L, M, n, ordering[sections])
  * (ldpc/sparc_ldpc.py:154-168; called with a fancy-indexed subset at

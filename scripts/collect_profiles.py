@@ -12,8 +12,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RND = sys.argv[1] if len(sys.argv) > 1 else "r04"
 # tag -> bench.py load_pmc key (workload_backend_precision_B)
 KEYS = {"c2": "c2_hadamard_fp32_B1", "c4b1": "c4_hadamard_fp32_B1", "c3": "c3_hadamard_fp32_B256",
-        "c4": "c4_hadamard_fp32_B256",
-        "dense_l768": "c4_dense_fp32_B1", "c3dense": "c3_dense_fp32_B256"}
+        "c4": "c4_hadamard_fp32_B256", "c2f64": "c2_hadamard_fp64_B1", "c3f64": "c3_hadamard_fp64_B256",
+        "c4f64": "c4_hadamard_fp64_B256", "joint": "c5_hadamard_fp64_B256",
+        "dense_l768": "c4_dense_fp32_B1", "c3dense": "c3_dense_fp32_B256",
+        "c2matrix": "c2_matrix_fp32_B1", "c3matrix": "c3_matrix_fp32_B256"}
 
 
 def main():
@@ -36,7 +38,7 @@ def main():
             subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "graph_trace.py"), tr,
                             os.path.join(dst, f"{RND}_{tag}_graph_trace.txt"), src], check=False,
                            stdout=subprocess.DEVNULL)
-    for tag in ("c2", "c3", "c3dense"):
+    for tag in ("c2", "c3", "c4", "c3dense"):
         p = os.path.join(out, f"sq_{tag}.txt")
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, f"{RND}_{tag}_sq_counters.txt"))
@@ -44,6 +46,9 @@ def main():
         p = os.path.join(out, f"stamps_{tag}.txt")
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, f"{RND}_{tag}_{kern}_stamps.txt"))
+    cal = os.path.join(out, "pmc_calib.json")
+    if os.path.exists(cal):
+        shutil.copy(cal, os.path.join(dst, f"{RND}_pmc_calib.json"))
     print(sorted(f for f in os.listdir(dst) if f.startswith(RND)))
 
 

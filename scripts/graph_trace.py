@@ -26,7 +26,7 @@ import sys
 sys.path.insert(0, __file__.rsplit("/", 1)[0])
 from pmc_summary import short  # noqa: E402
 
-LOOP = ("k_sec4", "k_sec43", "k_sec2", "k_sec", "k_secb", "k_row2", "k_rowv", "k_rowc", "k_row", "k_gemm_i8_Az", "k_gemm_i8_Ab",
+LOOP = ("k_sec4", "k_sec43", "k_sec2", "k_sec", "k_secb", "k_row2", "k_rowv", "k_rowc", "k_row", "k_gemm_i8_Az", "k_gemm_i8_Ab", "k_gemm_f_Az", "k_gemm_f_Ab",
         "k_dense_az", "k_dense_ab", "k_dense_den", "k_i8_quant")
 
 

@@ -8,6 +8,7 @@ fallback: without the library or a HIP device every call raises.
 """
 from ._lib import SparcAmpError, load as load_library
 from .operators import (SparcOperator, AbOp, AzOp, make_ordering, sub_fht, block_sub_fht, dense_transforms,
+                        gaussian_transforms,
                         sparc_transforms, sparc_transforms_shorter, default_device)
 from .amp import amp, amp_test, amp_batch, operator_of
 from .harness import (SPARCParams, LDPCParams, pa_parameterised, bits2indices, ber_of,

@@ -39,6 +39,7 @@ SA_PTR_DEVICE = 0x200
 SA_PLAN = {
     "SEC3": 1 << 0, "NO_SEC3": 1 << 1, "ROW16": 1 << 2, "NO_ROW16": 1 << 3, "NO_PT": 1 << 4,
     "ZIL": 1 << 5, "NO_ZIL": 1 << 6, "WB8": 1 << 7, "WB16": 1 << 8, "NO_BANKS": 1 << 9, "EAGER": 1 << 10,
+    "ONE_PASS": 1 << 11,
 }
 
 
@@ -60,7 +61,7 @@ def plan_bits(plan) -> int:
 
 # Every symbol include/sparc_amp.h declares (tests check the export table).
 EXPORTS = (
-    "sa_create", "sa_create_ex", "sa_create_matrix", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
+    "sa_create", "sa_create_ex", "sa_create_matrix", "sa_create_matrix_random", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
     "sa_reserve", "sa_stage", "sa_stage_power_batch", "sa_run", "sa_wait", "sa_fetch", "sa_fetch_z", "sa_run_event_ms",
     "sa_profile", "sa_profile_rep", "sa_profile_kinds", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
@@ -75,6 +76,7 @@ _SIG = {
     "sa_create": (_I, [ct.POINTER(_P), _I, _I, _I, ct.POINTER(ct.c_uint32), _I, _I, _I]),
     "sa_create_ex": (_I, [ct.POINTER(_P), _I, _I, _I, ct.POINTER(ct.c_uint32), _I, _I, _I, _I]),
     "sa_create_matrix": (_I, [ct.POINTER(_P), _I, _I, _I, _D, _I, _I]),
+    "sa_create_matrix_random": (_I, [ct.POINTER(_P), _I, _I, _I, ct.c_uint64, ct.c_double, _I, _I]),
     "sa_subset": (_I, [_P, ct.POINTER(ct.c_int64), _I, ct.POINTER(_P)]),
     "sa_destroy": (None, [_P]),
     "sa_Ab": (_I, [_P, _I, _D, _D]),

@@ -90,7 +90,8 @@ struct FAcc<double> {  // 2 x 4 tiles of 16 x 16 per wave
   f64x4 acc[2][4];
 };
 
-template <typename real>
+// AB: 0 for A^T z, 1 for A beta — the same code, two names in the profiles
+template <typename real, int AB>
 __global__ void __launch_bounds__(512) k_gemm_f(FArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int nb = gridDim.x, bid = blockIdx.x, per = nb / 8;
@@ -230,5 +231,55 @@ __global__ void __launch_bounds__(256) k_transpose(const real* __restrict__ A, l
   for (int jj = ty; jj < 64; jj += 4) {
     const long long j = j0 + jj, r = r0 + tx;
     if (j < rows_t && r < ld_t) AT[j * ld_t + r] = tile[tx][jj];
+  }
+}
+
+// ---- an i.i.d. Gaussian design generated on the device ----------------------
+// (sa_create_matrix_random: the design of a simulation that never needs it on
+// the host).  Philox4x32-10 (Salmon et al., SC'11) keyed by the seed, counter
+// = element index / 4; its four 32-bit words give two Box-Muller pairs, i.e.
+// four N(0, 1) values for four consecutive elements of a row-major n x (L*M)
+// matrix: reproducible per (seed, element) whatever the launch shape.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    const uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += W0;
+    key.y += W1;
+  }
+  return ctr;
+}
+
+template <typename real>
+__global__ void k_matrix_gauss(real* __restrict__ A, long long n, long long LM, size_t lda, unsigned long long seed,
+                               double scale) {
+  const long long total4 = (n * LM + 3) / 4;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < total4;
+       q += (long long)gridDim.x * blockDim.x) {
+    const uint4 w = philox4x32_10(make_uint4((uint32_t)q, (uint32_t)(q >> 32), 0u, 0u), key);
+    const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+    double g[4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const double u1 = ((double)u[2 * p] + 1.0) * (1.0 / 4294967296.0);  // (0, 1]
+      const double u2 = (double)u[2 * p + 1] * (1.0 / 4294967296.0);      // [0, 1)
+      const double rad = sqrt(-2.0 * log(u1));
+      double sn, cs;
+      sincospi(2.0 * u2, &sn, &cs);
+      g[2 * p] = rad * cs;
+      g[2 * p + 1] = rad * sn;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long e = q * 4 + i;
+      if (e < n * LM) {
+        const long long r = e / LM, j = e % LM;
+        A[(size_t)r * lda + (size_t)j] = (real)(g[i] * scale);
+      }
+    }
   }
 }

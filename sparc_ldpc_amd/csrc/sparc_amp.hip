@@ -775,6 +775,9 @@ struct SecArgs {
   // batched kernel: z and the Ab partials codeword-interleaved by chunk,
   // z [NC][n][CB] and abp [NC][G][n][CB] (16-byte rows, k_rowc), else [B][n] / [B][G][n]
   int zil;
+  // batched kernel: section groups per XCD per pass of the work order (the
+  // groups whose tables one XCD's L2 holds at a time); >= G / 8: one pass
+  int gpx;
   real sqrt_n;
 };
 
@@ -1717,6 +1720,8 @@ __global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real
 // workgroups of a section group are placed on one XCD (blockIdx % 8 labels
 // the XCD) so the group's tables stay in that XCD's L2.
 constexpr int kSG = 16;  // fwd table padding (sections)
+// table bytes of the section groups one XCD works on at a time (SecArgs::gpx)
+constexpr size_t kSecbL2 = (size_t)5 << 19;  // 2.5 MB of the 4 MB L2
 // sections (waves) per batched workgroup: 8 (two workgroups per CU), or 16
 // (one per CU) where the wider workgroup's LDS holds a larger codeword chunk
 // (sa_ctx::WB, chosen at context creation)
@@ -1850,12 +1855,19 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     const int bid = blockIdx.x, total = a.G * a.NC;
     if ((a.G & 7) == 0 && (total & 7) == 0) {
       const int x = bid & 7, j = bid >> 3;
-      // the XCD's G/8 section groups fastest: the workgroups in flight on
-      // one XCD (two per CU) cover G/8 groups' tables and a few codeword
-      // chunks' z, which stay in its L2 together
+      // the XCD's G/8 section groups in passes of gpx groups, the groups of
+      // a pass fastest: the workgroups in flight on one XCD cover the pass's
+      // tables and a few codeword chunks' z, which stay in its L2 together
+      // (C4: 6 groups' tables, 4.7 MB, overflowed the 4 MB L2; two passes of 3)
       const int gx = a.G >> 3;
-      g = (j % gx) * 8 + x;
-      chunk = j / gx;
+      int jj = j, g0 = 0, gp = a.gpx < gx ? a.gpx : gx;
+      while (jj >= gp * a.NC) {  // whole passes before this item (at most G / 8 steps)
+        jj -= gp * a.NC;
+        g0 += gp;
+        gp = gx - g0 < gp ? gx - g0 : gp;
+      }
+      g = (g0 + jj % gp) * 8 + x;
+      chunk = jj / gp;
     } else {
       g = bid / a.NC;
       chunk = bid % a.NC;
@@ -3023,6 +3035,7 @@ struct sa_ctx {
   int n_cus = 256;
   int Gb = 0, CB = 0;  // batched kernel: groups of WB sections, codewords per workgroup (0 = off)
   int WB = 8;          // batched kernel: sections per workgroup (kWB or kWB16)
+  int gpx = 1 << 20;   // batched kernel: section groups per XCD per pass (SecArgs::gpx)
   size_t secb_lds = 0;
   int RS = 1, KS = 1, Gd = 0;  // dense splits; Gd = dense denoiser groups
   size_t lda = 0;
@@ -3320,7 +3333,7 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   a.T1 = c->Tcap + 1; a.t = t; a.mode = mode; a.early_stop = early_stop;
   a.RS = 1;
   a.pt = 0;
-  a.B = 0; a.NC = 0; a.zil = 0;
+  a.B = 0; a.NC = 0; a.zil = 0; a.gpx = 1 << 20;
   a.cst = c->pb_on ? c->L : 0;
   if (c->pb_on) a.c = (const real*)c->d_cb;
   a.sqrt_n = (real)std::sqrt((double)c->n);
@@ -3370,6 +3383,7 @@ void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.B = B;
   a.NC = (B + CB - 1) / CB;
   a.zil = zil_for(c, B) ? 1 : 0;
+  a.gpx = c->gpx;
   if (c->prof) c->prof->begin(c->stream, K_SEC);
   const dim3 grid(c->Gb * a.NC);
   bool done = false;
@@ -3760,7 +3774,10 @@ int launch_gemm_f(sa_ctx* c, int B, const real* X, long long ldx, const real* Y,
   const long long grid = (long long)a.XT * a.YT * S;
   if (grid > 0x7fffffff) return fail(SA_ERR_UNSUPPORTED, "k_gemm_f: grid too large");
   if (c->prof) c->prof->begin(c->stream, kind);
-  PROF_REPS(c) k_gemm_f<real><<<(unsigned)grid, 512, kFLds, c->stream>>>(a);
+  if (kind == K_DAB)
+    PROF_REPS(c) k_gemm_f<real, 1><<<(unsigned)grid, 512, kFLds, c->stream>>>(a);
+  else
+    PROF_REPS(c) k_gemm_f<real, 0><<<(unsigned)grid, 512, kFLds, c->stream>>>(a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -4339,10 +4356,12 @@ int set_lds_limits() {
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)k_gemm_i8<kI8NPB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             I8Tile<kI8NPB>::Lds);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_gemm_f<float>, hipFuncAttributeMaxDynamicSharedMemorySize, kFLds);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_gemm_f<double>, hipFuncAttributeMaxDynamicSharedMemorySize, kFLds);
+  {
+    const void* fs[] = {(const void*)k_gemm_f<float, 0>, (const void*)k_gemm_f<float, 1>,
+                        (const void*)k_gemm_f<double, 0>, (const void*)k_gemm_f<double, 1>};
+    for (const void* f : fs)
+      if (e == hipSuccess) e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kFLds);
+  }
   if (e != hipSuccess) return fail(SA_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
   done = 1;
   return SA_OK;
@@ -4452,6 +4471,15 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     c->CB = c->WB == kWB16 ? c16.first : c8.first;
     c->secb_lds = c->WB == kWB16 ? c16.second : c8.second;
     c->Gb = (L + c->WB - 1) / c->WB;
+    // passes over each XCD's section groups so one pass's bucket and Ab
+    // tables (W sections x (w + n) x 2 B per group) stay within kSecbL2
+    // bytes of the XCD's 4 MB L2 (the rest: z chunks, streamed beta)
+    const size_t per_group = (size_t)c->WB * ((size_t)c->w + (size_t)n) * 2;
+    const int gx = c->Gb / 8 > 0 ? c->Gb / 8 : 1;
+    const int fit = (int)std::max<size_t>(1, kSecbL2 / per_group);
+    int npass = (gx + fit - 1) / fit;
+    c->gpx = (gx + npass - 1) / npass;  // balanced passes
+    if (plan & SA_PLAN_ONE_PASS) c->gpx = 1 << 20;
   }
   {
     hipDeviceProp_t prop;
@@ -4797,6 +4825,31 @@ int sa_create_matrix(sa_ctx** out, int L, int M, int n, const double* A, int pre
   if (rc) {
     sa_destroy(c);
     return rc;
+  }
+  *out = c;
+  return SA_OK;
+}
+
+int sa_create_matrix_random(sa_ctx** out, int L, int M, int n, uint64_t seed, double scale, int precision,
+                            int device) {
+  if (!out) return fail(SA_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (!std::isfinite(scale)) return fail(SA_ERR_ARG, "scale must be finite");
+  sa_ctx* c = nullptr;
+  int rc = create_impl(&c, L, M, n, nullptr, SA_BACKEND_MATRIX, precision, device, SA_PLAN_DEFAULT);
+  if (rc) return rc;
+  const long long LM = (long long)L * M;
+  if (c->prec == SA_PREC_F64)
+    k_matrix_gauss<double><<<8192, 256, 0, c->stream>>>((double*)c->d_A, n, LM, c->lda, (unsigned long long)seed,
+                                                         scale);
+  else
+    k_matrix_gauss<float><<<8192, 256, 0, c->stream>>>((float*)c->d_A, n, LM, c->lda, (unsigned long long)seed,
+                                                        scale);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    sa_destroy(c);
+    return fail(SA_ERR_HIP, std::string("k_matrix_gauss: ") + hipGetErrorString(e));
   }
   *out = c;
   return SA_OK;

@@ -20,7 +20,7 @@ from ._lib import as_f64, check, dptr
 
 __all__ = [
     "SparcOperator", "AbOp", "AzOp", "HostOperatorLoop", "make_ordering", "sub_fht", "block_sub_fht",
-    "sparc_transforms", "sparc_transforms_shorter", "dense_transforms", "default_device",
+    "sparc_transforms", "sparc_transforms_shorter", "dense_transforms", "gaussian_transforms", "default_device",
 ]
 
 _BACKENDS = {"hadamard": _lib.SA_BACKEND_HADAMARD, "dense": _lib.SA_BACKEND_DENSE}
@@ -147,6 +147,29 @@ class SparcOperator:
         self._ctx = _lib.ct.c_void_p()
         check(lib.sa_create_matrix(_lib.ct.byref(self._ctx), self.L, self.M, self.n, dptr(A), _PRECS[precision],
                                    self.device))
+        self._lib = lib
+        return self
+
+    @classmethod
+    def from_random(cls, L, M, n, seed=0, scale=None, precision=None, device=None):
+        """An i.i.d. N(0, scale²) design generated on the device (default
+        scale 1/√n): sa_create_matrix_random, Philox4x32-10 + Box–Muller,
+        reproducible per (seed, element)."""
+        lib = _lib.load()
+        precision = precision or DEFAULT_PRECISION
+        if precision not in _PRECS:
+            raise ValueError(f"precision must be one of {sorted(_PRECS)}")
+        self = cls.__new__(cls)
+        self.L, self.M, self.n = int(L), int(M), int(n)
+        self.w = None
+        self.backend, self.precision = "matrix", precision
+        self.device = default_device() if device is None else int(device)
+        self.ordering = None
+        self.plan_bits = 0
+        self.scale = float(1.0 / np.sqrt(n) if scale is None else scale)
+        self._ctx = _lib.ct.c_void_p()
+        check(lib.sa_create_matrix_random(_lib.ct.byref(self._ctx), self.L, self.M, self.n, int(seed) & (2**64 - 1),
+                                          self.scale, _PRECS[precision], self.device))
         self._lib = lib
         return self
 
@@ -530,6 +553,15 @@ def dense_transforms(A, L, M, *, precision=None, device=None):
     ``amp(y, σ, Pl, L, M, T, Ab, Az)`` keeps the whole loop on the device.
     Not cached: each call copies A to the device."""
     op = SparcOperator.from_matrix(A, L, M, precision=precision, device=device)
+    return AbOp(op), AzOp(op)
+
+
+def gaussian_transforms(L, M, n, seed=0, *, scale=None, precision=None, device=None):
+    """An i.i.d. Gaussian design N(0, scale²) (default scale 1/√n) generated on
+    the device: (Ab, Az) device operators for amp(), as dense_transforms()
+    gives for a host matrix.  The entries come from the device generator
+    (SparcOperator.from_random), not from NumPy's stream."""
+    op = SparcOperator.from_random(L, M, n, seed, scale, precision=precision, device=device)
     return AbOp(op), AzOp(op)
 
 

@@ -135,3 +135,38 @@ def test_matrix_refuses_ordering_only_entry_points(sp):
         op.subset([0, 1])
     with pytest.raises(AssertionError):
         sp.dense_transforms(A[:, :-1], 8, 16)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_device_gaussian_design(sp, prec):
+    """sa_create_matrix_random: the device-generated N(0, 1/n) design.  Its
+    columns (A e_j, through the GEMV and the GEMM paths alike) have the right
+    moments, the same seed gives the same matrix bit for bit and another seed
+    another one, A^T is the adjoint of A, and AMP over it recovers every
+    section at high SNR."""
+    L, M, n = 16, 64, 200
+    Ab, Az = sp.gaussian_transforms(L, M, n, seed=7, precision=prec)
+    op = Ab.op
+    E = np.eye(L * M)
+    cols = op.Ab_batch(E).T  # (n, L*M): column j = A e_j (GEMM path, B = L*M)
+    single = np.hstack([Ab(E[j].reshape(-1, 1)) for j in (0, 5, L * M - 1)])
+    assert np.array_equal(single, cols[:, [0, 5, L * M - 1]]) or rel(single, cols[:, [0, 5, L * M - 1]]) <= 1e-7
+    x = cols.reshape(-1) * np.sqrt(n)
+    assert abs(x.mean()) < 5 / np.sqrt(x.size) and abs(x.std() - 1) < 0.02
+    assert abs(np.mean(x ** 4) - 3) < 0.1  # Gaussian kurtosis
+    again = sp.SparcOperator.from_random(L, M, n, seed=7, precision=prec).Ab_batch(E[:8])
+    other = sp.SparcOperator.from_random(L, M, n, seed=8, precision=prec).Ab_batch(E[:8])
+    assert np.array_equal(again, cols[:, :8].T)
+    assert not np.allclose(other, again)
+    rs = np.random.RandomState(1)
+    z = rs.randn(n, 1)
+    assert rel(Az(z), cols.T @ z) <= OPTOL[prec] * 10
+    P = 2.0
+    Pl = P / L * np.ones(L)
+    idx = rs.randint(0, M, L)
+    b0 = np.zeros((L * M, 1)); b0[np.arange(L) * M + idx, 0] = np.sqrt(n * Pl)
+    y = Ab(b0) + 0.05 * rs.randn(n, 1)
+    b = sp.amp(y, 0, Pl, L, M, 30, Ab, Az)
+    assert np.array_equal(orc.section_argmax(b, L, M), idx)
+    ref = orc.amp(y, 0, Pl, L, M, 30, lambda v: cols @ v, lambda v: cols.T @ v)
+    assert rel(b, ref) <= 1e-4

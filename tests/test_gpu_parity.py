@@ -771,3 +771,23 @@ def test_fetch_z_layout_follows_every_run(sp):
     zb = op.fetch_z(B)
     assert np.array_equal(za, zb)
     assert rel(zb[0], z1[0]) <= 1e-4
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_batched_work_order_passes_bit_identical(sp, prec):
+    """C4 geometry (L = 768: 48 batched section groups, 6 per XCD): the
+    default work order in two passes of 3 groups per XCD (one pass's tables
+    fit the XCD's L2) and the single pass (plan option ONE_PASS) give the
+    same decode bit for bit (the placement changes no sum)."""
+    L, M = 768, 512
+    n = int(L * np.log2(M) / (5 / 6))
+    B, T, P = 8, 3, 1.8
+    oAb, _, oord = orc.sparc_transforms(L, M, n)
+    Pl = P / L * np.ones(L)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.6, oAb, 60 + i)[1].reshape(-1) for i in range(B)])
+    a = sp.SparcOperator(L, M, n, oord, precision=prec)
+    b = sp.SparcOperator(L, M, n, oord, precision=prec, plan="ONE_PASS")
+    assert a.plan(B)["section_kernel"] == "k_secb"
+    ba, ia = a.amp_batch(ys, Pl, T, early_stop=False)
+    bb, ib = b.amp_batch(ys, Pl, T, early_stop=False)
+    assert np.array_equal(ba, bb) and np.array_equal(ia, ib)

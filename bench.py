@@ -408,7 +408,7 @@ def timed_steps(op, B, T, steps, warmup):
     return mine, float(dist.allreduce_max(np.array([mine]))[0])
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -422,9 +422,17 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-dense", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0)
+    ap.add_argument("--cpu-iters", type=int, default=0,
+                    help="AMP iterations per CPU-baseline process (default: T, a whole decode)")
     ap.add_argument("--no-fp64", action="store_true", help="skip the binary64 leg of an fp32 run")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def main(argv=None, make_op=None):
+    """The bench; make_op(L, M, n, backend, precision, device, plan) replaces
+    the device operator (tests/test_bench_host.py drives the whole N-rank flow
+    on the CPU with a stand-in; the bench itself never passes one)."""
+    args = parse_args(argv)
     from sparc_ldpc_amd import dist
 
     rank, world, local = dist.env_rank()
@@ -438,7 +446,7 @@ def main():
     # one rank per GPU over RCCL (librccl through ctypes, no PyTorch); the
     # rehearsal mode SPARC_DIST_BACKEND=socket puts several ranks on one GPU
     # (device LOCAL_RANK % device count) with the CPU all-reduce instead
-    ndev = sp.load_library().sa_device_count()
+    ndev = sp.load_library().sa_device_count() if make_op is None else 1
     device = local % max(1, ndev) if os.environ.get("SPARC_DIST_BACKEND") == "socket" else local
     if world > 1:
         dist.init(device=device)
@@ -450,13 +458,15 @@ def main():
     L, M, P, T, B, sigma = w["L"], w["M"], w["P"], w["T"], w["B"], w["sigma"]
     n = n_of(w)
     Pl = P / L * np.ones(L)
-    if args.backend == "matrix":
+    plan = [p for p in args.plan.split(",") if p] or None
+    if make_op is not None:
+        op = make_op(L, M, n, args.backend, args.precision, device, plan)
+    elif args.backend == "matrix":
         op = sp.SparcOperator.from_random(L, M, n, seed=0, precision=args.precision, device=device)
         w["desc"] += "; i.i.d. Gaussian N(0, 1/n) design (device-generated), not the Hadamard operator"
     else:
         op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend=args.backend,
-                              precision=args.precision, device=device,
-                              plan=[p for p in args.plan.split(",") if p] or None)
+                              precision=args.precision, device=device, plan=plan)
     # per-rank synthetic reps: seeds 1000 + rank*B + i (sharded, no overlap)
     seeds = [1000 + rank * B + i for i in range(B)]
     y = synth_y(op, Pl, sigma, seeds)
@@ -495,8 +505,9 @@ def main():
         # the same workload in binary64 (the reference's precision; the joint
         # decoder's): same seeds, same timing protocol, every rank, with its
         # own live roofline
-        op64 = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="hadamard", precision="fp64",
-                                device=device)
+        op64 = (make_op(L, M, n, "hadamard", "fp64", device, None) if make_op is not None else
+                sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="hadamard", precision="fp64",
+                                 device=device))
         op64.reserve(B, T)
         op64.stage(y, Pl)
         _, e64 = timed_steps(op64, B, T, args.steps, args.warmup)
@@ -514,11 +525,12 @@ def main():
     if rank == 0 and not args.no_cpu:
         # after the timed region (every rank), on rank 0's host cores: the
         # N-rank line carries its own CPU baseline
-        result["cpu_baseline"] = cpu_baseline(w, args.cpu_procs or None)
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_procs or None, args.cpu_iters or None)
         result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.finalize()
+    return result
 
 
 if __name__ == "__main__":

@@ -81,8 +81,10 @@ int lb_wait(lb_ctx* ctx);
 int lb_fetch(lb_ctx* ctx, int B, double* app, int* iters);
 double lb_run_event_ms(lb_ctx* ctx);
 
-/* out[0..7] = Nv, Nc, Nmsg, max vdeg, max cdeg, messages in LDS (1/0),
- *             threads per workgroup, device */
+/* out[0..8] = Nv, Nc, Nmsg, max vdeg, max cdeg, messages in LDS (1/0),
+ *             threads per workgroup, device, and the check degree of the
+ *             straight-line check kernel of a check-regular code (0: the
+ *             general kernel) */
 int lb_info(lb_ctx* ctx, long long* out);
 int lb_device_count(void);
 const char* lb_last_error(void);

@@ -13,7 +13,8 @@ c = ldpc.code("802.16", "5/6", 192)
 lib = ldpc.load_bp_library()
 rs = np.random.RandomState(0)
 D = ct.POINTER(ct.c_double)
-for B in (1, 256, 1024):
+BS = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 256, 1024]
+for B in BS:
     for ebno in (3.0, 3.5, 4.5):
         U = rs.randint(0, 2, (B, c.K))
         X = c.encode_batch(U)

@@ -10,3 +10,7 @@ WORKLOADS="c4" bash scripts/ab.sh "--steps 20 --warmup 3 --no-fp64 --plan ONE_PA
 WORKLOADS="c3 c4" bash scripts/ab.sh "--steps 10 --warmup 2 --no-fp64 --precision fp64" $P $N || exit 1
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench_default.log; exit 1; }
 tail -1 gpurun_out/bench_default.log
+for lib in sparc_ldpc_amd/libldpc_bp_r03.so sparc_ldpc_amd/libldpc_bp.so; do
+  echo "BP $lib"; LDPC_BP_LIB=$lib timeout -k 10 200 python scripts/bp_time.py 1,256 || exit 1
+done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ldpc.py tests/test_gpu_joint.py -x -q --timeout 200 --timeout-method thread > gpurun_out/t_ldpc.log 2>&1; rc=$?; tail -3 gpurun_out/t_ldpc.log; exit $rc

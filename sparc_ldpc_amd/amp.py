@@ -13,6 +13,8 @@ exact-τ stop, η and the Onsager residual still run on the device
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 
 from .operators import AbOp, AzOp, SparcOperator, _cached_operator, host_loop
@@ -97,6 +99,9 @@ def _sibling(Ab, Az, precision):
     return AbOp(sib), AzOp(sib)
 
 
+_SWAP_WARNED = False
+
+
 def amp_test(y, σ_n, Pl, L, M, T, Ab, Az, β=None, *, early_stop=True, precision="fp64"):
     """amp_test.py:14-50 -> (β̂, t): t is the loop index at which the exact
     τ stop fired, or T-1 when the loop ran out (Python's loop variable).
@@ -117,6 +122,13 @@ def amp_test(y, σ_n, Pl, L, M, T, Ab, Az, β=None, *, early_stop=True, precisio
     if precision != "operator":
         sib = _sibling(Ab, Az, precision)
         if sib is not None:
+            global _SWAP_WARNED
+            if not _SWAP_WARNED:  # once per process: the swap changes the arithmetic and the cost
+                _SWAP_WARNED = True
+                warnings.warn(f"amp_test decodes a {Ab.op.precision} operator in {precision} (a cached twin of the "
+                              f"same design) so that its stop index follows the reference's binary64 "
+                              f"iterates; pass precision='operator' to keep the operator's own precision",
+                              stacklevel=2)
             Ab, Az = sib
     b, it = _run(y, Pl, L, M, T, Ab, Az, β, early_stop)
     return b, (it if it < T else T - 1)

@@ -103,6 +103,35 @@ __device__ __forceinline__ double lxfb(P L, int dc) {
   return lxor<CORR>(b, l0);
 }
 
+// Lxfb for checks of exactly DC edges (a check-regular code, e.g. 802.16
+// rate 5/6: dc = 20 everywhere), in the reference's own loop structure
+// (c_ldpc.c:294-314): the forward chain f[k] = Lxor(f[k-1], L[k]) and the
+// backward chain b[k] = Lxor(b[k+1], L[k]) run side by side, then every
+// output Lxor(f[k-1], b[k+1]) at once.  Straight-line code (no degree
+// guards), so the two dependent chains interleave: the critical path is
+// dc - 1 Lxor latencies plus one, against 2 (dc - 2) in lxfb's
+// forward-then-backward form.  The same operations on the same operands:
+// bit-identical to lxfb.
+template <int DC, bool CORR>
+__device__ __forceinline__ double lxfb_fixed(double* L) {
+  static_assert(DC >= 3, "fixed-degree checks");
+  double l[DC], f[DC - 1], b[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) l[k] = L[k];
+  f[0] = l[0];
+  b[DC - 1] = l[DC - 1];
+#pragma unroll
+  for (int k = 1; k < DC; ++k) {
+    if (k < DC - 1) f[k] = lxor<CORR>(f[k - 1], l[k]);  // f[DC-1] is never used
+    b[DC - 1 - k] = lxor<CORR>(b[DC - k], l[DC - 1 - k]);
+  }
+  L[0] = b[1];
+  L[DC - 1] = f[DC - 2];
+#pragma unroll
+  for (int k = 1; k < DC - 1; ++k) L[k] = lxor<CORR>(f[k - 1], b[k + 1]);
+  return b[0];  // = Lxor(b[1], L[0]), lxfb's return value
+}
+
 struct BpArgs {
   const double* ch;    // [B][Nv]
   double* app;         // [B][Nv]
@@ -115,8 +144,12 @@ struct BpArgs {
   double corr;
 };
 
-template <int ALGO, int DCMAX, bool LDSM>
-__global__ void __launch_bounds__(kMaxThreads) k_bp(BpArgs a) {
+// DCFIX > 0: every check node has exactly DCFIX edges (lxfb_fixed; launched
+// with at most kFixThreads threads, so a thread may hold the two chains in
+// registers: 3 waves per SIMD)
+constexpr int kFixThreads = 768;
+template <int ALGO, int DCMAX, bool LDSM, int DCFIX = 0>
+__global__ void __launch_bounds__(DCFIX > 0 ? kFixThreads : kMaxThreads) k_bp(BpArgs a) {
   extern __shared__ double lds_msg[];
   __shared__ int unsat[2];
   const int b = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
@@ -160,9 +193,11 @@ __global__ void __launch_bounds__(kMaxThreads) k_bp(BpArgs a) {
         bad = 2.0 * atanh(aggr) <= 0.0;
         for (int k = 0; k < dc; ++k) L[k] = 2.0 * atanh(aggr / L[k]);
       } else if (ALGO == LB_SUMPROD2) {  // c_ldpc.c:183-194
-        bad = lxfb<DCMAX, true>(L, dc) <= 0.0;
+        if constexpr (DCFIX > 0) bad = lxfb_fixed<DCFIX, true>(L) <= 0.0;
+        else bad = lxfb<DCMAX, true>(L, dc) <= 0.0;
       } else {  // minsum, c_ldpc.c:364-372 with node-aligned offsets
-        bad = lxfb<DCMAX, false>(L, dc) <= 0.0;
+        if constexpr (DCFIX > 0) bad = lxfb_fixed<DCFIX, false>(L) <= 0.0;
+        else bad = lxfb<DCMAX, false>(L, dc) <= 0.0;
         for (int k = 0; k < dc; ++k) L[k] *= a.corr;
       }
       if (bad) unsat[it & 1] = 1;
@@ -190,7 +225,12 @@ KernelFn pick_dc(int maxdc) {
   return k_bp<ALGO, 32, LDSM>;
 }
 
-KernelFn pick_kernel(int algo, int maxdc, bool lds) {
+// check-regular codes whose degree has a straight-line instance (lxfb_fixed)
+bool fixed_dc(int mindc, int maxdc, int nt) { return mindc == maxdc && maxdc == 20 && nt <= kFixThreads; }
+
+KernelFn pick_kernel(int algo, int maxdc, bool lds, bool fixed = false) {
+  if (fixed && algo == LB_SUMPROD2) return lds ? k_bp<LB_SUMPROD2, 32, true, 20> : k_bp<LB_SUMPROD2, 32, false, 20>;
+  if (fixed && algo == LB_MINSUM) return lds ? k_bp<LB_MINSUM, 32, true, 20> : k_bp<LB_MINSUM, 32, false, 20>;
   // sumprod does not use the register-resident forward values: one instance suffices
   switch (algo) {
     case LB_SUMPROD2: return lds ? pick_dc<LB_SUMPROD2, true>(maxdc) : pick_dc<LB_SUMPROD2, false>(maxdc);
@@ -214,7 +254,8 @@ int default_device() {
 }  // namespace
 
 struct lb_ctx {
-  int dev = 0, Nv = 0, Nc = 0, Nmsg = 0, maxdv = 0, maxdc = 0, nt = 0;
+  int dev = 0, Nv = 0, Nc = 0, Nmsg = 0, maxdv = 0, maxdc = 0, mindc = 0, nt = 0;
+  bool fixed = false;  // check-regular with a straight-line check kernel (lxfb_fixed)
   bool lds = false;
   int* d_vedge = nullptr;
   uint8_t* d_vdeg = nullptr;
@@ -284,7 +325,7 @@ int set_attrs(lb_ctx* c) {
   if (c->attrs_set || !c->lds) return LB_OK;
   const size_t bytes = (size_t)c->Nmsg * sizeof(double);
   for (int algo = 0; algo < 3; ++algo)
-    HIP_TRY(hipFuncSetAttribute((const void*)pick_kernel(algo, c->maxdc, true),
+    HIP_TRY(hipFuncSetAttribute((const void*)pick_kernel(algo, c->maxdc, true, c->fixed),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
   c->attrs_set = true;
   return LB_OK;
@@ -312,7 +353,7 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   a.maxit = max_iter;
   a.corr = corr;
   const size_t shm = c->lds ? (size_t)c->Nmsg * sizeof(double) : 0;
-  hipLaunchKernelGGL(pick_kernel(algo, c->maxdc, c->lds), dim3(B), dim3(c->nt), shm, c->stream, a);
+  hipLaunchKernelGGL(pick_kernel(algo, c->maxdc, c->lds, c->fixed), dim3(B), dim3(c->nt), shm, c->stream, a);
   HIP_TRY(hipGetLastError());
   return LB_OK;
 }
@@ -393,7 +434,7 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
     return fail(LB_ERR_ARG, "empty or null graph");
   // host-side validation (the reference trusts its own prepare_decoder)
   long sv = 0, sc = 0;
-  int maxdv = 0, maxdc = 0;
+  int maxdv = 0, maxdc = 0, mindc = 1 << 30;
   for (int j = 0; j < Nv; ++j) {
     if (vdeg[j] < 0) return fail(LB_ERR_GRAPH, "negative variable degree");
     sv += vdeg[j];
@@ -403,6 +444,7 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
     if (cdeg[j] < 1) return fail(LB_ERR_GRAPH, "check node of degree < 1");
     sc += cdeg[j];
     maxdc = cdeg[j] > maxdc ? (int)cdeg[j] : maxdc;
+    mindc = cdeg[j] < mindc ? (int)cdeg[j] : mindc;
   }
   if (sv != Nmsg || sc != Nmsg) return fail(LB_ERR_GRAPH, "sum(vdeg) and sum(cdeg) must equal Nmsg");
   if (maxdc > 32) return fail(LB_ERR_UNSUPPORTED, "check degree > 32");
@@ -437,6 +479,8 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   c->lds = (size_t)Nmsg * sizeof(double) <= kLdsBytes - 64;
   // one thread per check node when possible (the check phase dominates)
   c->nt = std::min(kMaxThreads, std::max(256, (Nc + 63) / 64 * 64));
+  c->mindc = mindc;
+  c->fixed = fixed_dc(mindc, maxdc, c->nt);
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };
   if (hipSetDevice(device) != hipSuccess) return bail(fail(LB_ERR_HIP, "hipSetDevice failed"));
@@ -547,6 +591,7 @@ int lb_info(lb_ctx* c, long long* out) {
   out[5] = c->lds ? 1 : 0;
   out[6] = c->nt;
   out[7] = c->dev;
+  out[8] = c->fixed ? c->maxdc : 0;
   return LB_OK;
 }
 

@@ -293,9 +293,9 @@ class code:
         return app[0], int(it[0])
 
     def info(self):
-        out = (ct.c_int64 * 8)()
+        out = (ct.c_int64 * 9)()
         _check(load_bp_library().lb_info(self._context(), out))
-        keys = ("Nv", "Nc", "Nmsg", "max_vdeg", "max_cdeg", "lds_messages", "threads", "device")
+        keys = ("Nv", "Nc", "Nmsg", "max_vdeg", "max_cdeg", "lds_messages", "threads", "device", "fixed_dc")
         return dict(zip(keys, list(out)))
 
     def Lxor(self, L1, L2, corrflag=1):

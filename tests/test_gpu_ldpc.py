@@ -71,6 +71,15 @@ def test_batch_equals_single_bitwise(bp):
         assert it == IT[b] and np.array_equal(a, A[b])
 
 
+def test_check_regular_code_runs_the_straight_line_check_kernel(bp):
+    """802.16 rate 5/6 (every check of degree 20, the joint decoder's outer
+    code) runs lxfb_fixed: the reference's forward / backward chains side by
+    side; the irregular rate-1/2 code keeps the general kernel.  Both are
+    checked against the reference C library in test_against_reference_library."""
+    assert bp.code("802.16", "5/6", 192).info()["fixed_dc"] == 20
+    assert bp.code("802.16", "1/2", 96).info()["fixed_dc"] == 0
+
+
 def test_batch_against_oracle(bp):
     c = bp.code("802.16", "5/6", 192)
     rs = np.random.RandomState(12)

@@ -82,7 +82,7 @@ enum {
   SA_PLAN_ROW16 = 1 << 2,     /* one codeword: 16-row k_row2 blocks where they fit */
   SA_PLAN_NO_ROW16 = 1 << 3,  /* one codeword: 32-row k_row2 blocks */
   SA_PLAN_NO_PT = 1 << 4,     /* Ab partials [G][n] instead of row-block major (bit-identical) */
-  SA_PLAN_ZIL = 1 << 5,       /* batched: z / Ab partials codeword-interleaved (binary64 too) */
+  SA_PLAN_ZIL = 1 << 5,       /* batched: z / Ab partials codeword-interleaved (the default since round 4) */
   SA_PLAN_NO_ZIL = 1 << 6,    /* batched: z / Ab partials [B][n] (binary32 too) */
   SA_PLAN_WB8 = 1 << 7,       /* batched: 8 sections per workgroup */
   SA_PLAN_WB16 = 1 << 8,      /* batched: 16 sections per workgroup */

@@ -126,6 +126,7 @@ def main():
     ap.add_argument("--ebno", type=float, default=6.888888888888889)
     ap.add_argument("--soft-iter", type=int, default=2)
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
+    ap.add_argument("--plan", default="", help="comma-separated plan options (sa_create_ex)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0)
     args = ap.parse_args()
@@ -138,6 +139,9 @@ def main():
     R = 5 / 6
     sigma = ebno_to_sigma(args.ebno, P, R)
     jd = joint.joint_decoder(L, M, N_SPARC, lp, T, precision=args.precision)
+    if args.plan:  # A/B of plan options: the same design with sa_create_ex options
+        jd.op = sp.SparcOperator(L, M, N_SPARC, sp.make_ordering(L, M, N_SPARC), precision=args.precision,
+                                 plan=[p for p in args.plan.split(",") if p])
     B = args.batch
     Pl = P / L * np.ones(L)
     idx, noise = jd.draw([np.random.RandomState(7000 + i) for i in range(B)], B, sigma)

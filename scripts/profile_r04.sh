@@ -7,7 +7,7 @@
 # summaries to profiles/r04_*.  Stops at the first step that fails.
 #   bash scripts/profile_r04.sh STEP ...
 #   steps: c2 c2f64 c4b1 c3 c3f64 c4 c4f64 joint dense_l768 c3dense c2matrix c3matrix
-#          sq_c2 sq_c3 sq_c4 sq_c3f64 calib
+#          sq_c2 sq_c3 sq_c4 sq_c3f64 sq_bp calib
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -41,6 +41,7 @@ for s in "$@"; do
     sq_c3) sq c3 --workload c3 --no-fp64 --steps 1 --warmup 0 ;;
     sq_c4) sq c4 --workload c4 --no-fp64 --steps 1 --warmup 0 ;;
     sq_c3f64) sq c3f64 --workload c3 --precision fp64 --steps 1 --warmup 0 ;;
+    sq_bp) SCRIPT=scripts/bp_time.py sq bp 256 ;;
     calib) bash scripts/calib_r04.sh || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -62,6 +62,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 using f4 = float __attribute__((ext_vector_type(4)));
+using d2v = double __attribute__((ext_vector_type(2)));
 
 
 
@@ -653,10 +654,12 @@ __device__ __forceinline__ void load_section(const real* p, real (&x)[E], int la
 }
 
 // Streaming (non-temporal) forms for beta in the batched kernel: read once
-// and written once per launch, 268 MB at c3, it otherwise sweeps each XCD's
-// 4 MB L2 and evicts the section tables and z that the XCD's workgroups
-// share (binary32 with 16-B vectors only: element-wise non-temporal
-// binary64 access measured 18% slower at c3)
+// and written once per launch, 268 MB at c3 (537 MB in binary64), it
+// otherwise sweeps each XCD's 4 MB L2 and evicts the section tables and z
+// that the XCD's workgroups share.  16-B vectors (binary64: two per group of
+// four elements; element-wise non-temporal binary64 access measured 18 %
+// slower at c3).  Only for the batched kernel's sections,
+// where E >= 4 means M = 64 E: every element of a lane's groups exists.
 template <typename real, int E>
 __device__ __forceinline__ void load_section_nt(const real* p, real (&x)[E], int lane, int M) {
   constexpr int Q = E < 4 ? E : 4;
@@ -665,6 +668,13 @@ __device__ __forceinline__ void load_section_nt(const real* p, real (&x)[E], int
     for (int i = 0; i < E; i += Q) {
       const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p + elem_index<E>(lane, i)));
       x[i] = t.x; x[i + 1] = t.y; x[i + 2] = t.z; x[i + 3] = t.w;
+    }
+  } else if constexpr (Q == 4 && sizeof(real) == 8) {
+#pragma unroll
+    for (int i = 0; i < E; i += Q) {
+      const d2v* q = reinterpret_cast<const d2v*>(p + elem_index<E>(lane, i));
+      const d2v t0 = __builtin_nontemporal_load(q), t1 = __builtin_nontemporal_load(q + 1);
+      x[i] = t0.x; x[i + 1] = t0.y; x[i + 2] = t1.x; x[i + 3] = t1.y;
     }
   } else {
     load_section<real, E>(p, x, lane, M);
@@ -678,6 +688,14 @@ __device__ __forceinline__ void store_section_nt(real* p, const real (&x)[E], in
     for (int i = 0; i < E; i += Q) {
       const f4 t = {x[i], x[i + 1], x[i + 2], x[i + 3]};
       __builtin_nontemporal_store(t, reinterpret_cast<f4*>(p + elem_index<E>(lane, i)));
+    }
+  } else if constexpr (Q == 4 && sizeof(real) == 8) {
+#pragma unroll
+    for (int i = 0; i < E; i += Q) {
+      d2v* q = reinterpret_cast<d2v*>(p + elem_index<E>(lane, i));
+      const d2v t0 = {x[i], x[i + 1]}, t1 = {x[i + 2], x[i + 3]};
+      __builtin_nontemporal_store(t0, q);
+      __builtin_nontemporal_store(t1, q + 1);
     }
   } else {
     store_section<real, E>(p, x, lane, M);
@@ -816,7 +834,6 @@ constexpr int kZU = 10;
 // (explicit members rather than an array: the array form was not promoted to
 // registers and its spill store waited for the loads at kernel start)
 #define SA_ZU_EACH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9)
-using d2v = double __attribute__((ext_vector_type(2)));
 template <typename real, int NT = 256>
 struct ZStage {
   // native vector types: HIP's float4 (a struct of unions) defeats SROA
@@ -1823,10 +1840,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   constexpr int NQ = (E + 3) / 4;
   // binary64: fewer loads in flight so a wave fits 128 VGPRs (two workgroups per CU)
   constexpr bool F64 = sizeof(real) == 8;
-  constexpr int KH = (E >= 16 || CB >= 4 || F64) ? 2 : 4;  // bucket h-steps with table loads in flight together
+  // bucket h-steps with table loads in flight together (binary64: one, which keeps
+  // the kernel within 128 VGPRs without spills: C3 fp64 +3.5 %)
+  constexpr int KH = F64 ? 1 : ((E >= 16 || CB >= 4) ? 2 : 4);
   // rows per thread whose Ab-table loads are in flight together (one with 16
   // sections at CB = 4: their 4 table words per row already fill the registers)
-  constexpr int KR = (CB >= 4 || F64) ? (W > 8 && CB >= 4 ? 1 : 2) : 3;
+  constexpr int KR = (CB >= 4 || F64) ? (W > 8 && (CB >= 4 || F64) ? 1 : 2) : 3;
   constexpr bool PB = CB <= 2 && !F64;           // prefetch the previous beta with the first loads
   constexpr int W4 = W / 4;             // 4-section table groups per workgroup
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -3526,11 +3545,13 @@ int launch_sec(sa_ctx* c, int B, int mode, int t, int es, void* bin = nullptr, v
 // their blocks cover the CUs twice, else k_row (64 rows).
 // The batched decode with z and the Ab partials interleaved by codeword chunk
 // (SecArgs::zil, 16-byte rows of CB codewords: binary32 CB = 4, binary64
-// CB = 2), row kernel k_rowc.  Default in binary32 (C3 +1.7 %, C4 +4.7 %);
-// binary64 only with the plan option SA_PLAN_ZIL (its k_secb spills 68 bytes
-// against 36: C3 -1.6 %, the joint decode -1.5 %); SA_PLAN_NO_ZIL keeps [B][n]
+// CB = 2), row kernel k_rowc.  The default in binary32 (C3 +1.7 %, C4
+// +4.7 %) and, since the binary64 k_secb no longer spills (round 4: one
+// bucket h-step in flight, 16-byte non-temporal beta), in binary64 too (C3
+// 6.30 k -> 6.44 k, C4 3.09-3.12 k -> 3.19 k cw/s; round 3's spilling kernel
+// lost 1.6 %); SA_PLAN_NO_ZIL keeps [B][n]
 bool zil_for(const sa_ctx* c, int B) {
-  const bool on = (c->plan & SA_PLAN_ZIL) ? true : (c->plan & SA_PLAN_NO_ZIL) ? false : c->prec == SA_PREC_F32;
+  const bool on = (c->plan & SA_PLAN_NO_ZIL) ? false : true;
   return on && c->backend == SA_BACKEND_HADAMARD && use_batched(c, B) && c->CB * (int)rsz(c) == 16;
 }
 
@@ -4449,10 +4470,11 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   // 8-section workgroups share a CU (CB = 1 takes the whole LDS if it must);
   // one 16-section workgroup per CU instead where its whole-LDS image holds a
   // larger chunk (L = 768, n = 8294: CB 4 instead of 2; binary64 2 instead of
-  // 1), and in binary32 also at equal CB (half the Ab partials: the row
-  // kernel's HBM read halves, the section kernel pays a 16-wave barrier):
-  // C4 batch 256 4.45 k -> 5.51 k cw/s (binary64 2.17 k -> 2.41 k), C3
-  // 11.10 k -> 11.26 k.  SPARC_AMP_WB=8/16 forces the width.
+  // 1), and also at equal CB (half the Ab partials: the row kernel's HBM read
+  // halves, the section kernel pays a 16-wave barrier): C4 batch 256 4.45 k
+  // -> 5.51 k cw/s (binary64 2.17 k -> 2.41 k), C3 11.10 k -> 11.26 k; in
+  // binary64 at equal CB since round 4 (C3 fp64 with ZIL 6.44 k -> 7.02 k,
+  // the joint configs[4] step 1.65 k -> 1.75 k).  SA_PLAN_WB8 / WB16 force it.
   {
     auto cb_for = [&](int W) -> std::pair<int, size_t> {
       for (int cb = (s == 4 ? 4 : 2); cb >= 1 && M <= 1024; cb >>= 1) {
@@ -4466,7 +4488,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     const auto c8 = cb_for(kWB), c16 = cb_for(kWB16);
     const bool w16 = (plan & SA_PLAN_WB16) ? true
                      : (plan & SA_PLAN_WB8) ? false
-                                            : (c16.first > c8.first || (s == 4 && c16.first == c8.first));
+                                            : c16.first >= c8.first;
     c->WB = w16 && c16.first > 0 ? kWB16 : kWB;
     c->CB = c->WB == kWB16 ? c16.first : c8.first;
     c->secb_lds = c->WB == kWB16 ? c16.second : c8.second;
@@ -4476,7 +4498,9 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     // bytes of the XCD's 4 MB L2 (the rest: z chunks, streamed beta)
     const size_t per_group = (size_t)c->WB * ((size_t)c->w + (size_t)n) * 2;
     const int gx = c->Gb / 8 > 0 ? c->Gb / 8 : 1;
-    const int fit = (int)std::max<size_t>(1, kSecbL2 / per_group);
+    size_t l2 = kSecbL2;
+    if (const char* e = getenv("SPARC_AMP_SECB_L2_KB")) l2 = (size_t)std::max(1, atoi(e)) << 10;  // measurement only
+    const int fit = (int)std::max<size_t>(1, l2 / per_group);
     int npass = (gx + fit - 1) / fit;
     c->gpx = (gx + npass - 1) / npass;  // balanced passes
     if (plan & SA_PLAN_ONE_PASS) c->gpx = 1 << 20;

@@ -306,12 +306,12 @@ def test_batch_matches_single_and_deterministic(sp, prec, L, M, B):
                                              ("fp64", 1025, "k_row", "0"), ("fp32", 1024, "k_rowc", "1"),
                                              ("fp32", 1025, "k_rowc", "1"), ("fp64", 1026, "k_rowc", "1"),
                                              ("fp64", 1025, "k_rowc", "1"), ("fp32", 1024, "k_rowc", None),
-                                             ("fp64", 1026, "k_rowv16B", None)])
+                                             ("fp64", 1026, "k_rowc", None)])
 def test_row_kernel_variants_vs_oracle(sp, prec, n, want, zil):
     """Every batched row kernel (the Onsager residual of sparc_ldpc.py:220 and
     the A beta sum of :143-146): with z and the Ab partials codeword-interleaved
-    (k_rowc: the binary32 default, binary64 with plan option ZIL) and, with
-    NO_ZIL (the binary64 default), k_rowv with 16-byte rows (binary32 n % 4 == 0, binary64 n
+    (k_rowc: the default in both precisions) and, with
+    NO_ZIL, k_rowv with 16-byte rows (binary32 n % 4 == 0, binary64 n
     even), with 8-byte rows (binary32 n even), k_row for odd n; each chosen at
     B = 128 and checked against the oracle codeword by codeword."""
     L, M, B, P, T = 128, 256, 128, 2.0, 4

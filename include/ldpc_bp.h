@@ -63,7 +63,8 @@ int lb_decode(lb_ctx* ctx, int B, const double* ch, double* app, int* iters, int
               double corr_factor, int max_iter);
 
 /* Device-resident form: d_ch / d_app / d_iters are device pointers on the
- * context's device; runs on the context's stream and returns without waiting. */
+ * context's device; runs on the context's stream and returns without waiting
+ * (but for the tail's one read-back, see lb_set_tail). */
 int lb_decode_device(lb_ctx* ctx, int B, const double* d_ch, double* d_app, int* d_iters, int algo,
                      double corr_factor, int max_iter);
 
@@ -81,11 +82,20 @@ int lb_wait(lb_ctx* ctx);
 int lb_fetch(lb_ctx* ctx, int B, double* app, int* iters);
 double lb_run_event_ms(lb_ctx* ctx);
 
-/* out[0..8] = Nv, Nc, Nmsg, max vdeg, max cdeg, messages in LDS (1/0),
- *             threads per workgroup, device, and the check degree of the
+/* out[0..9] = Nv, Nc, Nmsg, max vdeg, max cdeg, messages in LDS (1/0),
+ *             threads per workgroup, device, the check degree of the
  *             straight-line check kernel of a check-regular code (0: the
- *             general kernel) */
+ *             general kernel), and the first tail iteration (0: off) */
 int lb_info(lb_ctx* ctx, long long* out);
+
+/* Tail launches: a decode runs its first `tail_at` iterations one workgroup
+ * per word; the words still running after that are spread over several
+ * workgroups each, one launch per iteration (bit-identical results; the run
+ * reads back the number of words left once, so lb_decode_device / lb_run
+ * wait for the first phase when max_iter > tail_at).  tail_at < 0: the
+ * default (8, or the environment's LDPC_BP_TAIL at lb_create); 0: off.
+ * Needs variable degrees <= 12 (LB_ERR_UNSUPPORTED otherwise). */
+int lb_set_tail(lb_ctx* ctx, int tail_at);
 int lb_device_count(void);
 const char* lb_last_error(void);
 const char* lb_version(void);

@@ -1,8 +1,9 @@
 #!/bin/bash
 # Every bench line of the round (GPU box): the default headline (c2, with the
 # CPU baseline and the dense GEMV probe), c3, c4 (256 reps), c4 single
-# codeword, the dense backend at c3 (int8 MFMA GEMMs) and c4 single (fp32
-# GEMVs), and a 2-rank rehearsal of the N-rank path on one GPU over the
+# codeword, binary64 c3 / c4, the dense backend at c3 (int8 MFMA GEMMs) and
+# c4 single (fp32 GEMVs), a caller's Gaussian design (matrix backend) at c2 /
+# c3, the joint configs[4] step (scripts/bench_joint.py), and a 2-rank rehearsal of the N-rank path on one GPU over the
 # socket all-reduce.  Lines land in gpurun_out/bench_<tag>.json.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -17,8 +18,15 @@ b c2
 b c3 --workload c3 --no-cpu --no-dense
 b c4 --workload c4 --no-cpu --no-dense
 b c4b1 --workload c4 --batch 1 --no-cpu --no-dense
+b c3f64 --workload c3 --precision fp64 --no-fp64 --no-cpu --no-dense
+b c4f64 --workload c4 --precision fp64 --no-fp64 --no-cpu --no-dense --steps 10 --warmup 2
 b c3dense --workload c3 --backend dense --no-cpu --no-dense --steps 5 --warmup 1
 b c4b1dense --workload c4 --batch 1 --backend dense --no-cpu --no-dense --steps 3 --warmup 1
+b c2matrix --backend matrix --no-cpu --no-dense --no-fp64 --steps 5 --warmup 1
+b c3matrix --workload c3 --backend matrix --no-cpu --no-dense --no-fp64 --steps 2 --warmup 1
+timeout -k 10 600 python scripts/bench_joint.py > gpurun_out/bench_joint.log 2>&1 || { echo "joint failed"; tail -5 gpurun_out/bench_joint.log; exit 1; }
+grep '^{' gpurun_out/bench_joint.log | tail -1 > gpurun_out/bench_joint.json
+python3 -c "import json; d=json.load(open('gpurun_out/bench_joint.json')); print('joint', d['value'], d['ms_per_step'], d['step_share_ms'], d['cpu_baseline']['value'])"
 SPARC_DIST_BACKEND=socket timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --no-fp64 \
   > gpurun_out/bench_c2_rehearse_socket2.log 2>&1 || { echo "rehearsal failed"; tail -20 gpurun_out/bench_c2_rehearse_socket2.log; exit 1; }

@@ -113,11 +113,9 @@ __device__ __forceinline__ double lxfb(P L, int dc) {
 // forward-then-backward form.  The same operations on the same operands:
 // bit-identical to lxfb.
 template <int DC, bool CORR>
-__device__ __forceinline__ double lxfb_fixed(double* L) {
+__device__ __forceinline__ double lxfb_fixed_regs(const double (&l)[DC], double (&o)[DC]) {
   static_assert(DC >= 3, "fixed-degree checks");
-  double l[DC], f[DC - 1], b[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) l[k] = L[k];
+  double f[DC - 1], b[DC];
   f[0] = l[0];
   b[DC - 1] = l[DC - 1];
 #pragma unroll
@@ -125,11 +123,47 @@ __device__ __forceinline__ double lxfb_fixed(double* L) {
     if (k < DC - 1) f[k] = lxor<CORR>(f[k - 1], l[k]);  // f[DC-1] is never used
     b[DC - 1 - k] = lxor<CORR>(b[DC - k], l[DC - 1 - k]);
   }
-  L[0] = b[1];
-  L[DC - 1] = f[DC - 2];
+  o[0] = b[1];
+  o[DC - 1] = f[DC - 2];
 #pragma unroll
-  for (int k = 1; k < DC - 1; ++k) L[k] = lxor<CORR>(f[k - 1], b[k + 1]);
+  for (int k = 1; k < DC - 1; ++k) o[k] = lxor<CORR>(f[k - 1], b[k + 1]);
   return b[0];  // = Lxor(b[1], L[0]), lxfb's return value
+}
+
+template <int DC, bool CORR>
+__device__ __forceinline__ double lxfb_fixed(double* L) {
+  double l[DC], o[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) l[k] = L[k];
+  const double r = lxfb_fixed_regs<DC, CORR>(l, o);
+#pragma unroll
+  for (int k = 0; k < DC; ++k) L[k] = o[k];
+  return r;
+}
+
+// One check node's rule on its dc messages at L (in place): the reference's
+// three decoders.  Returns whether the check is unsatisfied (the stopping rule).
+template <int ALGO, int DCMAX, int DCFIX, typename P>
+__device__ __forceinline__ bool check_rule(P L, int dc, double corr) {
+  bool bad;
+  if (ALGO == LB_SUMPROD) {  // c_ldpc.c:76-102
+    double aggr = 1.0;
+    for (int k = 0; k < dc; ++k) {
+      const double t = tanh(L[k] / 2.0);
+      L[k] = t;
+      aggr *= t;
+    }
+    bad = 2.0 * atanh(aggr) <= 0.0;
+    for (int k = 0; k < dc; ++k) L[k] = 2.0 * atanh(aggr / L[k]);
+  } else if (ALGO == LB_SUMPROD2) {  // c_ldpc.c:183-194
+    if constexpr (DCFIX > 0) bad = lxfb_fixed<DCFIX, true>(L) <= 0.0;
+    else bad = lxfb<DCMAX, true>(L, dc) <= 0.0;
+  } else {  // minsum, c_ldpc.c:364-372 with node-aligned offsets
+    if constexpr (DCFIX > 0) bad = lxfb_fixed<DCFIX, false>(L) <= 0.0;
+    else bad = lxfb<DCMAX, false>(L, dc) <= 0.0;
+    for (int k = 0; k < dc; ++k) L[k] *= corr;
+  }
+  return bad;
 }
 
 struct BpArgs {
@@ -142,6 +176,14 @@ struct BpArgs {
   const int* cstart;   // [Nc+1] first message of each check node
   int Nv, Nc, Nmsg, maxit;
   double corr;
+  // hand-off to the tail kernels (tail != 0): a word not converged after
+  // maxit iterations leaves its messages in gmsg and its index in active[]
+  int tail;
+  int* active;   // [B]
+  int* nactive;  // [1]
+  int* done;     // [B]
+  int* lastbad;  // [2][B]: iteration stamp of the last unsatisfied check, by parity
+  int B;
 };
 
 // DCFIX > 0: every check node has exactly DCFIX edges (lxfb_fixed; launched
@@ -181,31 +223,154 @@ __global__ void __launch_bounds__(DCFIX > 0 ? kFixThreads : kMaxThreads) k_bp(Bp
     // check nodes
     for (int c = tid; c < Nc; c += nt) {
       const int s = a.cstart[c], dc = a.cstart[c + 1] - s;
-      double* L = msg + s;
-      bool bad;
-      if (ALGO == LB_SUMPROD) {  // c_ldpc.c:76-102
-        double aggr = 1.0;
-        for (int k = 0; k < dc; ++k) {
-          const double t = tanh(L[k] / 2.0);
-          L[k] = t;
-          aggr *= t;
-        }
-        bad = 2.0 * atanh(aggr) <= 0.0;
-        for (int k = 0; k < dc; ++k) L[k] = 2.0 * atanh(aggr / L[k]);
-      } else if (ALGO == LB_SUMPROD2) {  // c_ldpc.c:183-194
-        if constexpr (DCFIX > 0) bad = lxfb_fixed<DCFIX, true>(L) <= 0.0;
-        else bad = lxfb<DCMAX, true>(L, dc) <= 0.0;
-      } else {  // minsum, c_ldpc.c:364-372 with node-aligned offsets
-        if constexpr (DCFIX > 0) bad = lxfb_fixed<DCFIX, false>(L) <= 0.0;
-        else bad = lxfb<DCMAX, false>(L, dc) <= 0.0;
-        for (int k = 0; k < dc; ++k) L[k] *= a.corr;
-      }
+      const bool bad = check_rule<ALGO, DCMAX, DCFIX>(msg + s, dc, a.corr);
       if (bad) unsat[it & 1] = 1;
     }
     __syncthreads();
     if (!unsat[it & 1]) break;  // c_ldpc.c:196-197
   }
-  if (tid == 0) a.iters[b] = it;
+  if (a.tail && it == a.maxit) {
+    // not converged in the first maxit iterations: the messages go to the
+    // word's slice of gmsg (already there without LDS) for k_bp_tail
+    if (LDSM) {
+      double* g = a.gmsg + (size_t)b * a.Nmsg;
+      for (int i = tid; i < a.Nmsg; i += nt) g[i] = msg[i];
+    }
+    if (tid == 0) {
+      a.active[atomicAdd(a.nactive, 1)] = b;
+      a.done[b] = 0;
+      a.lastbad[((it - 1) & 1) * a.B + b] = it - 1;  // iteration it-1 left a check unsatisfied
+      a.lastbad[(it & 1) * a.B + b] = -1;            // no stale stamp from an earlier decode
+    }
+  } else if (tid == 0) {
+    a.iters[b] = it;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tail: the iterations after the first `tail_at`, for the words still running
+// ---------------------------------------------------------------------------
+// One workgroup holds one word's whole decode above, so the words that do not
+// converge (at the joint simulator's operating point a fifth of them run to
+// max_iter) leave most of the chip idle while the launch waits for them: each
+// iteration is a fixed ~75 us of one CU's binary64 VALU.  From iteration
+// tail_at on, the words still running are spread over the chip, two launches
+// per iteration, messages in HBM in two slots (read r_{t-1}, write r_t):
+//   k_bp_tail_var: thread per variable node, ch + incoming messages in port
+//     order (c_ldpc.c:171-178) -> app[v] (the aggregate itself);
+//   k_bp_tail_chk: S workgroups per word, thread per check node, input
+//     app[v(e)] - r_{t-1}[e] (the reference's extrinsic, the same subtraction)
+//     and the check rule of k_bp.
+// Bit-identical to running the whole decode in k_bp.
+struct TailArgs {
+  const double* ch;      // [B][Nv]
+  double* app;           // [B][Nv]
+  int* iters;            // [B]
+  const double* rold;    // [B][Nmsg] check-to-variable messages of iteration it-1
+  double* rnew;          // [B][Nmsg] ... of iteration it
+  const int* vedge;      // [maxdv][Nv]
+  const uint8_t* vdeg;   // [Nv]
+  const int* evar;       // [Nmsg] variable node of each edge
+  const int* cstart;     // [Nc+1]
+  const int* active;     // [n] words still running
+  int* done;             // [B]
+  int* ndone;            // [1] words detected as done in the tail (the host's stop test)
+  int* lastbad;          // [2][B]
+  int Nv, Nc, Nmsg, B, n, S, it;
+  double corr;
+};
+
+// DV >= the largest variable degree (4, 8 or 12): every port's table entry
+// and message loaded at once, summed in port order with exact selects
+template <int DV>
+__global__ void __launch_bounds__(256) k_bp_tail_var(TailArgs a) {
+  const int wi = blockIdx.y;
+  const int w = a.active[wi];
+  if (a.done[w]) return;  // converged in an earlier iteration
+  if (a.lastbad[((a.it - 1) & 1) * a.B + w] != a.it - 1) {
+    // iteration it-1 satisfied every check (c_ldpc.c:196-197): it is the word's last
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      a.iters[w] = a.it - 1;
+      a.done[w] = 1;
+      atomicAdd(a.ndone, 1);
+    }
+    return;
+  }
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.Nv) return;
+  const double* rold = a.rold + (size_t)w * a.Nmsg;
+  const int d = a.vdeg[j];
+  int e[DV];
+#pragma unroll
+  for (int k = 0; k < DV; ++k) e[k] = a.vedge[(size_t)(k < d ? k : 0) * a.Nv + j];
+  double x[DV];
+#pragma unroll
+  for (int k = 0; k < DV; ++k) x[k] = rold[e[k]];
+  double aggr = a.ch[(size_t)w * a.Nv + j];
+#pragma unroll
+  for (int k = 0; k < DV; ++k)
+    if (k < d) aggr += x[k];
+  a.app[(size_t)w * a.Nv + j] = aggr;
+}
+
+constexpr int kTailFixThreads = 256, kTailThreads = 128;
+template <int ALGO, int DCMAX, int DCFIX>
+__global__ void __launch_bounds__(DCFIX > 0 ? kTailFixThreads : kTailThreads) k_bp_tail_chk(TailArgs a) {
+  constexpr int ROW = DCMAX + 1;
+  __shared__ double rows[DCFIX > 0 ? 1 : kTailThreads * ROW];
+  const int wi = blockIdx.x / a.S, slice = blockIdx.x % a.S;
+  if (wi >= a.n) return;
+  const int w = a.active[wi];
+  if (a.done[w]) return;
+  const double* rold = a.rold + (size_t)w * a.Nmsg;
+  double* rnew = a.rnew + (size_t)w * a.Nmsg;
+  const double* app = a.app + (size_t)w * a.Nv;
+  const int cpw = (a.Nc + a.S - 1) / a.S;
+  const int c0 = slice * cpw, c1 = min(a.Nc, c0 + cpw);
+  bool anybad = false;
+  for (int c = c0 + (int)threadIdx.x; c < c1; c += blockDim.x) {
+    if constexpr (DCFIX > 0) {
+      const int s = c * DCFIX;  // check-regular: cstart[c] = c * DCFIX
+      int ev[DCFIX];
+      double r[DCFIX], l[DCFIX], o[DCFIX];
+#pragma unroll
+      for (int k = 0; k < DCFIX; ++k) {
+        ev[k] = a.evar[s + k];
+        r[k] = rold[s + k];
+      }
+#pragma unroll
+      for (int k = 0; k < DCFIX; ++k) l[k] = app[ev[k]] - r[k];
+      bool bad;
+      if (ALGO == LB_SUMPROD2) {
+        bad = lxfb_fixed_regs<DCFIX, true>(l, o) <= 0.0;
+      } else {
+        bad = lxfb_fixed_regs<DCFIX, false>(l, o) <= 0.0;
+#pragma unroll
+        for (int k = 0; k < DCFIX; ++k) o[k] *= a.corr;
+      }
+#pragma unroll
+      for (int k = 0; k < DCFIX; ++k) rnew[s + k] = o[k];
+      anybad |= bad;
+    } else {
+      const int s = a.cstart[c], dc = a.cstart[c + 1] - s;
+      double* L = rows + threadIdx.x * ROW;
+      for (int k = 0; k < dc; ++k) L[k] = app[a.evar[s + k]] - rold[s + k];
+      anybad |= check_rule<ALGO, DCMAX, 0>(L, dc, a.corr);
+      for (int k = 0; k < dc; ++k) rnew[s + k] = L[k];
+    }
+  }
+  if (anybad) a.lastbad[(a.it & 1) * a.B + w] = a.it;
+}
+
+// after the last tail iteration: the iteration count of the words that ran to
+// the end (max_iter, or max_iter - 1 when the last iteration converged)
+__global__ void k_bp_tail_end(int* iters, const int* active, const int* nactive, const int* done,
+                              const int* lastbad, int B, int maxit) {
+  const int n = *nactive;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int w = active[i];
+    if (!done[w]) iters[w] = lastbad[((maxit - 1) & 1) * B + w] == maxit - 1 ? maxit : maxit - 1;
+  }
 }
 
 __global__ void k_lxor(double a, double b, int corr, double* out) {
@@ -239,6 +404,33 @@ KernelFn pick_kernel(int algo, int maxdc, bool lds, bool fixed = false) {
   }
 }
 
+using TailFn = void (*)(TailArgs);
+
+template <int ALGO>
+TailFn pick_tail_dc(int maxdc) {
+  if (maxdc <= 8) return k_bp_tail_chk<ALGO, 8, 0>;
+  if (maxdc <= 16) return k_bp_tail_chk<ALGO, 16, 0>;
+  return k_bp_tail_chk<ALGO, 32, 0>;
+}
+
+TailFn pick_tail(int algo, int maxdc, bool fixed) {
+  if (fixed && algo == LB_SUMPROD2) return k_bp_tail_chk<LB_SUMPROD2, 32, 20>;
+  if (fixed && algo == LB_MINSUM) return k_bp_tail_chk<LB_MINSUM, 32, 20>;
+  switch (algo) {
+    case LB_SUMPROD2: return pick_tail_dc<LB_SUMPROD2>(maxdc);
+    case LB_SUMPROD: return pick_tail_dc<LB_SUMPROD>(maxdc);
+    default: return pick_tail_dc<LB_MINSUM>(maxdc);
+  }
+}
+
+TailFn pick_tail_var(int nq) {
+  return nq == 1 ? k_bp_tail_var<4> : (nq == 2 ? k_bp_tail_var<8> : k_bp_tail_var<12>);
+}
+
+// first iteration of the tail launches (0: off); LDPC_BP_TAIL overrides
+constexpr int kTailAt = 8;
+constexpr int kTailChunk = 8;  // tail iterations per stop test
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -257,6 +449,13 @@ struct lb_ctx {
   int dev = 0, Nv = 0, Nc = 0, Nmsg = 0, maxdv = 0, maxdc = 0, mindc = 0, nt = 0;
   bool fixed = false;  // check-regular with a straight-line check kernel (lxfb_fixed)
   bool lds = false;
+  // tail launches (k_bp_tail): edge tables, per-word state, first tail iteration
+  int tail_at = 0, nq = 0, ncu = 256;
+  int* d_evar = nullptr;
+  int *d_active = nullptr, *d_nact = nullptr, *d_done = nullptr, *d_lastbad = nullptr;
+  int* h_nact = nullptr;  // pinned: [0] words entering the tail, [1..2] done counts of the last chunks
+  hipEvent_t evc[2] = {nullptr, nullptr};
+  int capTailB = 0;
   int* d_vedge = nullptr;
   uint8_t* d_vdeg = nullptr;
   int* d_cstart = nullptr;
@@ -280,6 +479,14 @@ void release(lb_ctx* c) {
   (void)hipFree(c->d_app);
   (void)hipFree(c->d_msg);
   (void)hipFree(c->d_it);
+  (void)hipFree(c->d_evar);
+  (void)hipFree(c->d_active);
+  (void)hipFree(c->d_nact);
+  (void)hipFree(c->d_done);
+  (void)hipFree(c->d_lastbad);
+  if (c->h_nact) (void)hipHostFree(c->h_nact);
+  for (hipEvent_t e : c->evc)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -310,14 +517,42 @@ int ensure_io(lb_ctx* c, int B) {
   return LB_OK;
 }
 
-int ensure_msg(lb_ctx* c, int B) {
-  if (c->lds || B <= c->capMsgB) return LB_OK;
+// message slices: one per word without LDS, two per word (r_{t-1}, r_t)
+// for the tail launches; capMsgB counts word slices
+int ensure_msg(lb_ctx* c, int B, bool tail) {
+  const int need = tail ? 2 * B : (c->lds ? 0 : B);
+  if (need <= c->capMsgB) return LB_OK;
   (void)hipFree(c->d_msg);
   c->d_msg = nullptr;
   c->capMsgB = 0;
   int rc;
-  if ((rc = dev_alloc((void**)&c->d_msg, (size_t)B * c->Nmsg * sizeof(double)))) return rc;
-  c->capMsgB = B;
+  if ((rc = dev_alloc((void**)&c->d_msg, (size_t)need * c->Nmsg * sizeof(double)))) return rc;
+  c->capMsgB = need;
+  return LB_OK;
+}
+
+int ensure_tail(lb_ctx* c, int B) {
+  if (B <= c->capTailB) return LB_OK;
+  (void)hipFree(c->d_active);
+  (void)hipFree(c->d_done);
+  (void)hipFree(c->d_lastbad);
+  c->d_active = c->d_done = c->d_lastbad = nullptr;
+  c->capTailB = 0;
+  int rc;
+  if ((rc = dev_alloc((void**)&c->d_active, (size_t)B * sizeof(int)))) return rc;
+  if ((rc = dev_alloc((void**)&c->d_done, (size_t)B * sizeof(int)))) return rc;
+  if ((rc = dev_alloc((void**)&c->d_lastbad, (size_t)2 * B * sizeof(int)))) return rc;
+  if (!c->d_nact && (rc = dev_alloc((void**)&c->d_nact, 2 * sizeof(int)))) return rc;
+  for (hipEvent_t& e : c->evc)
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      e = nullptr;
+      return fail(LB_ERR_HIP, "hipEventCreate failed");
+    }
+  if (!c->h_nact && hipHostMalloc((void**)&c->h_nact, 3 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+    c->h_nact = nullptr;
+    return fail(LB_ERR_NOMEM, "hipHostMalloc failed");
+  }
+  c->capTailB = B;
   return LB_OK;
 }
 
@@ -336,9 +571,11 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   if (algo < LB_SUMPROD2 || algo > LB_MINSUM) return fail(LB_ERR_ARG, "unknown decoder type");
   if (max_iter < 0) return fail(LB_ERR_ARG, "max_iter < 0");
   if (B == 0) return LB_OK;
+  const bool tail = c->tail_at > 0 && max_iter > c->tail_at;
   int rc;
-  if ((rc = ensure_msg(c, B))) return rc;
+  if ((rc = ensure_msg(c, B, tail))) return rc;
   if ((rc = set_attrs(c))) return rc;
+  if (tail && (rc = ensure_tail(c, B))) return rc;
   BpArgs a;
   a.ch = d_ch;
   a.app = d_app;
@@ -350,10 +587,77 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   a.Nv = c->Nv;
   a.Nc = c->Nc;
   a.Nmsg = c->Nmsg;
-  a.maxit = max_iter;
+  a.maxit = tail ? c->tail_at : max_iter;
   a.corr = corr;
+  a.tail = tail ? 1 : 0;
+  a.active = c->d_active;
+  a.nactive = c->d_nact;
+  a.done = c->d_done;
+  a.lastbad = c->d_lastbad;
+  a.B = B;
+  if (tail) HIP_TRY(hipMemsetAsync(c->d_nact, 0, 2 * sizeof(int), c->stream));  // nactive, ndone
   const size_t shm = c->lds ? (size_t)c->Nmsg * sizeof(double) : 0;
   hipLaunchKernelGGL(pick_kernel(algo, c->maxdc, c->lds, c->fixed), dim3(B), dim3(c->nt), shm, c->stream, a);
+  HIP_TRY(hipGetLastError());
+  if (!tail) return LB_OK;
+
+  // how many words are left decides the tail's shape (one 4-byte read-back)
+  HIP_TRY(hipMemcpyAsync(c->h_nact, c->d_nact, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const int n = *c->h_nact;
+  if (n < 0 || n > B) return fail(LB_ERR_HIP, "tail word count out of range");
+  if (n == 0) return LB_OK;
+  // m waves per workgroup so that the n words' waves (one thread per check)
+  // cover the SIMDs once: S = ceil(Nc / 64m) workgroups per word
+  const long waves = (long)n * ((c->Nc + 63) / 64);
+  const int mmax = c->fixed && algo != LB_SUMPROD ? kTailFixThreads / 64 : kTailThreads / 64;
+  int m = (int)((waves + 4L * c->ncu - 1) / (4L * c->ncu));
+  m = m < 1 ? 1 : (m > mmax ? mmax : m);
+  const int S = (c->Nc + 64 * m - 1) / (64 * m);
+  TailArgs t;
+  t.ch = d_ch;
+  t.app = d_app;
+  t.iters = d_it;
+  t.vedge = c->d_vedge;
+  t.vdeg = c->d_vdeg;
+  t.evar = c->d_evar;
+  t.cstart = c->d_cstart;
+  t.active = c->d_active;
+  t.done = c->d_done;
+  t.ndone = c->d_nact + 1;
+  t.lastbad = c->d_lastbad;
+  t.Nv = c->Nv;
+  t.Nc = c->Nc;
+  t.Nmsg = c->Nmsg;
+  t.B = B;
+  t.n = n;
+  t.S = S;
+  t.corr = corr;
+  double* slot[2] = {c->d_msg, c->d_msg + (size_t)B * c->Nmsg};
+  const TailFn chk = pick_tail(algo, c->maxdc, c->fixed && algo != LB_SUMPROD);
+  const TailFn var = pick_tail_var(c->nq);
+  const dim3 vgrid((c->Nv + 255) / 256, n);
+  // chunks of kTailChunk iterations; after each, the count of words found
+  // done is copied back, and the host stops issuing chunks once the copy of
+  // two chunks ago shows every word done (the GPU keeps the latest chunk
+  // meanwhile: no stall while words run, no empty launches to max_iter after)
+  for (int it0 = c->tail_at, k = 0; it0 < max_iter; it0 += kTailChunk, ++k) {
+    if (k >= 2) {
+      HIP_TRY(hipEventSynchronize(c->evc[k & 1]));
+      if (c->h_nact[1 + (k & 1)] >= n) break;
+    }
+    for (int it = it0; it < std::min(max_iter, it0 + kTailChunk); ++it) {
+      t.rold = slot[(it - c->tail_at) & 1];
+      t.rnew = slot[(it - c->tail_at + 1) & 1];
+      t.it = it;
+      hipLaunchKernelGGL(var, vgrid, dim3(256), 0, c->stream, t);
+      hipLaunchKernelGGL(chk, dim3((unsigned)n * S), dim3(64 * m), 0, c->stream, t);
+    }
+    HIP_TRY(hipMemcpyAsync(c->h_nact + 1 + (k & 1), c->d_nact + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->evc[k & 1], c->stream));
+  }
+  hipLaunchKernelGGL(k_bp_tail_end, dim3((n + 255) / 256), dim3(256), 0, c->stream, d_it, c->d_active, c->d_nact,
+                     c->d_done, c->d_lastbad, B, max_iter);
   HIP_TRY(hipGetLastError());
   return LB_OK;
 }
@@ -468,6 +772,15 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   }
   cs[0] = 0;
   for (int j = 0; j < Nc; ++j) cs[j + 1] = cs[j] + (int)cdeg[j];
+  // tail edge table: the variable node of each edge
+  const int nq = maxdv <= 12 ? std::max(1, (maxdv + 3) / 4) : 0;
+  std::vector<int> evar;
+  if (nq) {
+    evar.resize(Nmsg);
+    long q = 0;
+    for (int j = 0; j < Nv; ++j)
+      for (int k = 0; k < vdeg[j]; ++k) evar[intrlv[q++]] = j;
+  }
 
   lb_ctx* c = new lb_ctx;
   c->dev = device;
@@ -481,12 +794,23 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   c->nt = std::min(kMaxThreads, std::max(256, (Nc + 63) / 64 * 64));
   c->mindc = mindc;
   c->fixed = fixed_dc(mindc, maxdc, c->nt);
+  c->nq = nq;
+  c->tail_at = 0;
+  if (c->nq) {
+    const char* e = getenv("LDPC_BP_TAIL");
+    c->tail_at = (e && *e) ? std::max(0, atoi(e)) : kTailAt;
+  }
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };
   if (hipSetDevice(device) != hipSuccess) return bail(fail(LB_ERR_HIP, "hipSetDevice failed"));
   if ((rc = dev_alloc((void**)&c->d_vedge, vedge.size() * sizeof(int)))) return bail(rc);
   if ((rc = dev_alloc((void**)&c->d_vdeg, (size_t)Nv))) return bail(rc);
   if ((rc = dev_alloc((void**)&c->d_cstart, (size_t)(Nc + 1) * sizeof(int)))) return bail(rc);
+  if (c->nq && (rc = dev_alloc((void**)&c->d_evar, evar.size() * sizeof(int)))) return bail(rc);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(LB_ERR_HIP, "stream/event creation failed"));
@@ -495,6 +819,7 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   if (hipMemcpyAsync(c->d_vedge, vedge.data(), vedge.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(c->d_vdeg, vd.data(), (size_t)Nv, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(c->d_cstart, cs.data(), (size_t)(Nc + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      (c->nq && hipMemcpyAsync(c->d_evar, evar.data(), evar.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return bail(fail(LB_ERR_HIP, "graph upload failed"));
   *out = c;
@@ -592,6 +917,14 @@ int lb_info(lb_ctx* c, long long* out) {
   out[6] = c->nt;
   out[7] = c->dev;
   out[8] = c->fixed ? c->maxdc : 0;
+  out[9] = c->tail_at;
+  return LB_OK;
+}
+
+int lb_set_tail(lb_ctx* c, int tail_at) {
+  if (!c) return fail(LB_ERR_ARG, "null context");
+  if (tail_at > 0 && !c->nq) return fail(LB_ERR_UNSUPPORTED, "tail launches need variable degrees <= 12");
+  c->tail_at = tail_at < 0 ? (c->nq ? kTailAt : 0) : tail_at;
   return LB_OK;
 }
 

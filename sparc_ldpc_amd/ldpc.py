@@ -32,7 +32,7 @@ EXPORTS = (
     "sumprod", "sumprod2", "minsum", "Lxor", "Lxfb",
     "lb_create", "lb_destroy", "lb_decode", "lb_decode_device", "lb_stage", "lb_run", "lb_wait",
     "lb_fetch", "lb_run_event_ms", "lb_info", "lb_device_count", "lb_last_error", "lb_version",
-    "lb_buffers",
+    "lb_buffers", "lb_set_tail",
 )
 
 _P, _I, _D = ct.c_void_p, ct.c_int, ct.POINTER(ct.c_double)
@@ -54,6 +54,7 @@ _SIG = {
     "lb_fetch": (_I, [_P, _I, _D, ct.POINTER(ct.c_int)]),
     "lb_run_event_ms": (ct.c_double, [_P]),
     "lb_info": (_I, [_P, ct.POINTER(ct.c_int64)]),
+    "lb_set_tail": (_I, [_P, _I]),
     "lb_device_count": (_I, []),
     "lb_last_error": (ct.c_char_p, []),
     "lb_version": (ct.c_char_p, []),
@@ -79,7 +80,9 @@ def load_bp_library(path: str = LIB_PATH) -> ct.CDLL:
                           "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = ct.CDLL(path)
     for name, (res, args) in _SIG.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an older build (A/B runs): the entry point stays absent
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib
@@ -293,10 +296,17 @@ class code:
         return app[0], int(it[0])
 
     def info(self):
-        out = (ct.c_int64 * 9)()
+        out = (ct.c_int64 * 10)()
         _check(load_bp_library().lb_info(self._context(), out))
-        keys = ("Nv", "Nc", "Nmsg", "max_vdeg", "max_cdeg", "lds_messages", "threads", "device", "fixed_dc")
+        keys = ("Nv", "Nc", "Nmsg", "max_vdeg", "max_cdeg", "lds_messages", "threads", "device", "fixed_dc",
+                "tail_at")
         return dict(zip(keys, list(out)))
+
+    def set_tail(self, tail_at=-1):
+        """First iteration of the tail launches (words still running after it
+        are spread over several workgroups each; bit-identical).  -1: the
+        default, 0: off (include/ldpc_bp.h lb_set_tail)."""
+        _check(load_bp_library().lb_set_tail(self._context(), int(tail_at)))
 
     def Lxor(self, L1, L2, corrflag=1):
         """ldpc.py:932-935 (evaluated on the GPU)."""

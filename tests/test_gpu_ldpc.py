@@ -173,3 +173,43 @@ def test_max_iter_and_errors(bp):
         c.decode(np.zeros(c.N + 1))
     with pytest.raises(NameError):
         c.decode(CH[0], "bitflip")
+
+
+@pytest.mark.parametrize("std,rate,z,ebno", [("802.16", "5/6", 192, 3.2), ("802.11n", "1/2", 81, 1.2),
+                                             ("802.16", "1/2", 96, 1.3), ("802.16", "5/6", 300, 3.2)])
+def test_tail_launches_bit_identical(bp, std, rate, z, ebno):
+    """The tail launches (words still running after tail_at iterations spread
+    over several workgroups, one launch per iteration, the variable update
+    folded into the check kernel) against whole decodes in one workgroup per
+    word: app and iteration counts identical for every word, every decoder,
+    with words that stop before, at and after the hand-off and words that run
+    to max_iter; the straight-line (5/6), general (1/2: variable degrees up to
+    11 and 6) and HBM-message (z = 300) kernels."""
+    c = bp.code(std, rate, z)
+    rs = np.random.RandomState(18)
+    X, CH = _awgn(c, rs, ebno, 24)
+    CH[:4] = 10 * (0.5 - X[:4])  # stop at iteration 0
+    algos = ["sumprod2", "sumprod"] + (["minsum"] if len(set(c.cdeg.tolist())) == 1 else [])
+    try:
+        for algo in algos:
+            c.set_tail(0)
+            assert c.info()["tail_at"] == 0
+            for mi in (200, 9):
+                A0, I0 = c.decode_batch(CH, algo, max_iter=mi)
+                if mi == 200:
+                    its = I0
+                for at in (1, 3, 8):
+                    c.set_tail(at)
+                    A1, I1 = c.decode_batch(CH, algo, max_iter=mi)
+                    assert np.array_equal(I0, I1), (algo, mi, at)
+                    # sumprod's tanh product saturates (atanh(+-1) = +-inf, then inf - inf) on words
+                    # that do not converge: NaN in both, at the same places
+                    assert np.array_equal(A0, A1, equal_nan=True), (
+                        algo, mi, at, np.isnan(A0).sum(), np.isnan(A1).sum(),
+                        np.nanmax(np.abs(np.where(np.isnan(A0) | np.isnan(A1), 0, A0 - A1))))
+                c.set_tail(0)
+            if algo == "sumprod2":
+                assert (its > 8).any() and (its < 3).any()  # words on both sides of the hand-off
+    finally:
+        c.set_tail(-1)
+    assert c.info()["tail_at"] == 8

@@ -63,13 +63,46 @@ constexpr size_t kLdsBytes = 160 * 1024;
 // Lxor (c_ldpc.c:234-251): sign product times min |.|, plus the two
 // log(1+exp(-|.|)) corrections for the exact sum-product rule.  Symmetric in
 // its arguments, bit for bit.
+//
+// The logarithm's argument is 1 + exp(-|x|), in [1, 2]: log12 evaluates it in
+// the structure of fdlibm's e_log.c (u = 2^k m, m in [sqrt(2)/2, sqrt(2)],
+// f = m - 1 exact, s = f / (2 + f), log(1 + f) = f - hfsq + s (hfsq + R(s^2)),
+// |error| < 1 ulp) instead of ROCm's general log, whose double-double steps
+// cost 46 of the 224 instructions of an Lxor: the check kernels are bound by
+// this arithmetic.  Against glibc's log on the arguments Lxor produces (u = 1
+// + exp(-x), x in [0, 40], 2e7 samples) 0.51 % of the results differ, by one
+// ulp, never more (the reference's own build differs from ROCm's log by last
+// ulps as well).  -DLB_OCML_LOG restores ROCm's log.
+__host__ __device__ __forceinline__ double log12(double u) {
+#ifdef LB_OCML_LOG
+  return log(u);
+#else
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+               Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  // branch-free: k = 0 gives 0 - ((hfsq - (s (hfsq + R) + 0)) - f), which is
+  // e_log.c's f - (hfsq - s (hfsq + R)) bit for bit (f = m - 1 is never -0)
+  const double k = u > 1.41421356237309504880 ? 1.0 : 0.0;
+  const double m = u * (1.0 - 0.5 * k);
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+  const double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  return k * ln2_hi - ((hfsq - (s * (hfsq + R) + k * ln2_lo)) - f);
+#endif
+}
+
 template <bool CORR>
 __device__ __forceinline__ double lxor(double a, double b) {
   double L = (signbit(a) == signbit(b)) ? 1.0 : -1.0;
   L *= fmin(fabs(a), fabs(b));
   if (CORR) {
-    L += log(1.0 + exp(-fabs(a + b)));
-    L -= log(1.0 + exp(-fabs(a - b)));
+    L += log12(1.0 + exp(-fabs(a + b)));
+    L -= log12(1.0 + exp(-fabs(a - b)));
   }
   return L;
 }
@@ -271,6 +304,8 @@ struct TailArgs {
   const int* vedge;      // [maxdv][Nv]
   const uint8_t* vdeg;   // [Nv]
   const int* evar;       // [Nmsg] variable node of each edge
+  const int* evd;        // [Nmsg] variable node | its degree << 24 (k_bp_tail_fused)
+  const int4* eadj;      // [Nmsg] that variable's edges in port order, padded with the edge itself
   const int* cstart;     // [Nc+1]
   const int* active;     // [n] words still running
   int* done;             // [B]
@@ -311,6 +346,78 @@ __global__ void __launch_bounds__(256) k_bp_tail_var(TailArgs a) {
   for (int k = 0; k < DV; ++k)
     if (k < d) aggr += x[k];
   a.app[(size_t)w * a.Nv + j] = aggr;
+}
+
+// Check-regular codes with variable degrees <= 4 (802.16 rate 5/6): the
+// variable update folded into the check kernel, one launch per iteration.  A
+// check thread loads its DC edges' variable tables, then every incoming
+// message of those variables at once (DC x 4 gathers in flight: one wave per
+// SIMD has the registers), and sums ch[v] + the messages in port order for
+// each edge (the adds of k_bp_tail_var, in the same order); the thread of a
+// variable's port-0 edge writes app[v].  One wave per workgroup, S =
+// ceil(Nc / 64) workgroups per word.
+template <int ALGO, int DC>
+__global__ void __launch_bounds__(64) k_bp_tail_fused(TailArgs a) {
+  const int wi = blockIdx.x / a.S, slice = blockIdx.x % a.S;
+  if (wi >= a.n) return;
+  const int w = a.active[wi];
+  if (a.done[w]) return;  // converged in an earlier iteration
+  if (a.lastbad[((a.it - 1) & 1) * a.B + w] != a.it - 1) {
+    // iteration it-1 satisfied every check (c_ldpc.c:196-197): it is the word's last
+    if (slice == 0 && threadIdx.x == 0) {
+      a.iters[w] = a.it - 1;
+      a.done[w] = 1;
+      atomicAdd(a.ndone, 1);
+    }
+    return;
+  }
+  const int c = slice * 64 + (int)threadIdx.x;
+  if (c >= a.Nc) return;
+  const double* rold = a.rold + (size_t)w * a.Nmsg;
+  double* rnew = a.rnew + (size_t)w * a.Nmsg;
+  const double* ch = a.ch + (size_t)w * a.Nv;
+  double* app = a.app + (size_t)w * a.Nv;
+  const int s = c * DC;  // check-regular: cstart[c] = c * DC
+  int vd[DC];
+  int4 adj[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    vd[k] = a.evd[s + k];
+    adj[k] = a.eadj[s + k];
+  }
+  double x0[DC], x1[DC], x2[DC], x3[DC], cv[DC], r[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    r[k] = rold[s + k];
+    cv[k] = ch[vd[k] & 0xffffff];
+    x0[k] = rold[adj[k].x];
+    x1[k] = rold[adj[k].y];
+    x2[k] = rold[adj[k].z];
+    x3[k] = rold[adj[k].w];
+  }
+  double l[DC], o[DC];
+#pragma unroll
+  for (int k = 0; k < DC; ++k) {
+    const int d = (int)((unsigned)vd[k] >> 24);
+    double aggr = cv[k];
+    if (0 < d) aggr += x0[k];
+    if (1 < d) aggr += x1[k];
+    if (2 < d) aggr += x2[k];
+    if (3 < d) aggr += x3[k];
+    if (adj[k].x == s + k) app[vd[k] & 0xffffff] = aggr;
+    l[k] = aggr - r[k];
+  }
+  bool bad;
+  if (ALGO == LB_SUMPROD2) {
+    bad = lxfb_fixed_regs<DC, true>(l, o) <= 0.0;
+  } else {
+    bad = lxfb_fixed_regs<DC, false>(l, o) <= 0.0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) o[k] *= a.corr;
+  }
+#pragma unroll
+  for (int k = 0; k < DC; ++k) rnew[s + k] = o[k];
+  if (bad) a.lastbad[(a.it & 1) * a.B + w] = a.it;
 }
 
 constexpr int kTailFixThreads = 256, kTailThreads = 128;
@@ -451,7 +558,10 @@ struct lb_ctx {
   bool lds = false;
   // tail launches (k_bp_tail): edge tables, per-word state, first tail iteration
   int tail_at = 0, nq = 0, ncu = 256;
+  bool tail_fuse = true;  // k_bp_tail_fused where it applies (LDPC_BP_TAIL_FUSE=0: two kernels)
   int* d_evar = nullptr;
+  int* d_evd = nullptr;   // k_bp_tail_fused tables (variable degrees <= 4)
+  int* d_eadj = nullptr;
   int *d_active = nullptr, *d_nact = nullptr, *d_done = nullptr, *d_lastbad = nullptr;
   int* h_nact = nullptr;  // pinned: [0] words entering the tail, [1..2] done counts of the last chunks
   hipEvent_t evc[2] = {nullptr, nullptr};
@@ -480,6 +590,8 @@ void release(lb_ctx* c) {
   (void)hipFree(c->d_msg);
   (void)hipFree(c->d_it);
   (void)hipFree(c->d_evar);
+  (void)hipFree(c->d_evd);
+  (void)hipFree(c->d_eadj);
   (void)hipFree(c->d_active);
   (void)hipFree(c->d_nact);
   (void)hipFree(c->d_done);
@@ -611,8 +723,10 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   // cover the SIMDs once: S = ceil(Nc / 64m) workgroups per word
   const long waves = (long)n * ((c->Nc + 63) / 64);
   const int mmax = c->fixed && algo != LB_SUMPROD ? kTailFixThreads / 64 : kTailThreads / 64;
+  // check-regular, variable degrees <= 4: one fused launch per iteration, one wave per workgroup
+  const bool fused = c->tail_fuse && c->d_evd && c->fixed && algo != LB_SUMPROD && c->maxdc == 20;
   int m = (int)((waves + 4L * c->ncu - 1) / (4L * c->ncu));
-  m = m < 1 ? 1 : (m > mmax ? mmax : m);
+  m = fused || m < 1 ? 1 : (m > mmax ? mmax : m);
   const int S = (c->Nc + 64 * m - 1) / (64 * m);
   TailArgs t;
   t.ch = d_ch;
@@ -621,6 +735,8 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.vedge = c->d_vedge;
   t.vdeg = c->d_vdeg;
   t.evar = c->d_evar;
+  t.evd = c->d_evd;
+  t.eadj = reinterpret_cast<const int4*>(c->d_eadj);
   t.cstart = c->d_cstart;
   t.active = c->d_active;
   t.done = c->d_done;
@@ -634,7 +750,8 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.S = S;
   t.corr = corr;
   double* slot[2] = {c->d_msg, c->d_msg + (size_t)B * c->Nmsg};
-  const TailFn chk = pick_tail(algo, c->maxdc, c->fixed && algo != LB_SUMPROD);
+  const TailFn chk = fused ? (algo == LB_SUMPROD2 ? k_bp_tail_fused<LB_SUMPROD2, 20> : k_bp_tail_fused<LB_MINSUM, 20>)
+                           : pick_tail(algo, c->maxdc, c->fixed && algo != LB_SUMPROD);
   const TailFn var = pick_tail_var(c->nq);
   const dim3 vgrid((c->Nv + 255) / 256, n);
   // chunks of kTailChunk iterations; after each, the count of words found
@@ -650,7 +767,7 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
       t.rold = slot[(it - c->tail_at) & 1];
       t.rnew = slot[(it - c->tail_at + 1) & 1];
       t.it = it;
-      hipLaunchKernelGGL(var, vgrid, dim3(256), 0, c->stream, t);
+      if (!fused) hipLaunchKernelGGL(var, vgrid, dim3(256), 0, c->stream, t);
       hipLaunchKernelGGL(chk, dim3((unsigned)n * S), dim3(64 * m), 0, c->stream, t);
     }
     HIP_TRY(hipMemcpyAsync(c->h_nact + 1 + (k & 1), c->d_nact + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -774,12 +891,25 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   for (int j = 0; j < Nc; ++j) cs[j + 1] = cs[j] + (int)cdeg[j];
   // tail edge table: the variable node of each edge
   const int nq = maxdv <= 12 ? std::max(1, (maxdv + 3) / 4) : 0;
-  std::vector<int> evar;
+  std::vector<int> evar, evd, eadj;
   if (nq) {
     evar.resize(Nmsg);
     long q = 0;
     for (int j = 0; j < Nv; ++j)
       for (int k = 0; k < vdeg[j]; ++k) evar[intrlv[q++]] = j;
+  }
+  if (nq == 1 && Nv < (1 << 24)) {  // k_bp_tail_fused: per edge its variable (| degree << 24) and that variable's edges
+    evd.resize(Nmsg);
+    eadj.resize((size_t)Nmsg * 4);
+    long q = 0;
+    for (int j = 0; j < Nv; ++j) {
+      for (int k = 0; k < vdeg[j]; ++k) {
+        const int e = (int)intrlv[q + k];
+        evd[e] = j | (int)(vdeg[j] << 24);
+        for (int p = 0; p < 4; ++p) eadj[(size_t)e * 4 + p] = p < vdeg[j] ? (int)intrlv[q + p] : e;
+      }
+      q += vdeg[j];
+    }
   }
 
   lb_ctx* c = new lb_ctx;
@@ -799,6 +929,8 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   if (c->nq) {
     const char* e = getenv("LDPC_BP_TAIL");
     c->tail_at = (e && *e) ? std::max(0, atoi(e)) : kTailAt;
+    const char* f = getenv("LDPC_BP_TAIL_FUSE");
+    c->tail_fuse = !(f && *f == '0');
   }
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };
@@ -807,6 +939,9 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   if ((rc = dev_alloc((void**)&c->d_vdeg, (size_t)Nv))) return bail(rc);
   if ((rc = dev_alloc((void**)&c->d_cstart, (size_t)(Nc + 1) * sizeof(int)))) return bail(rc);
   if (c->nq && (rc = dev_alloc((void**)&c->d_evar, evar.size() * sizeof(int)))) return bail(rc);
+  if (!evd.empty() && ((rc = dev_alloc((void**)&c->d_evd, evd.size() * sizeof(int))) ||
+                       (rc = dev_alloc((void**)&c->d_eadj, eadj.size() * sizeof(int)))))
+    return bail(rc);
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
@@ -820,6 +955,8 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
       hipMemcpyAsync(c->d_vdeg, vd.data(), (size_t)Nv, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(c->d_cstart, cs.data(), (size_t)(Nc + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       (c->nq && hipMemcpyAsync(c->d_evar, evar.data(), evar.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
+      (!evd.empty() && (hipMemcpyAsync(c->d_evd, evd.data(), evd.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+                        hipMemcpyAsync(c->d_eadj, eadj.data(), eadj.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess)) ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return bail(fail(LB_ERR_HIP, "graph upload failed"));
   *out = c;

@@ -263,6 +263,8 @@ PROFILE_TAGS = {  # (workload, codewords, backend, precision) -> scripts/profile
     ("c3", 256, "hadamard", "fp32"): "c3", ("c4", 256, "hadamard", "fp32"): "c4",
     ("c3", 256, "dense", "fp32"): "c3dense", ("c4", 1, "dense", "fp32"): "dense_l768",
     ("c2", 1, "hadamard", "fp64"): "c2f64", ("c3", 256, "hadamard", "fp64"): "c3f64",
+    ("c4", 256, "hadamard", "fp64"): "c4f64", ("c2", 1, "matrix", "fp32"): "c2matrix",
+    ("c3", 256, "matrix", "fp32"): "c3matrix",
 }
 
 

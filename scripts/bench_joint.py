@@ -179,6 +179,9 @@ def main():
     kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}[dom]
     achieved = per[dom] / (kinds_rep[dom][0] * 1e-3) / 1e9
     pmc = load_pmc(f"c5_hadamard_{args.precision}_B{B}", kname)
+    from sparc_ldpc_amd._lib import source_hash
+    src = source_hash()
+    fresh = pmc is not None and pmc.get("sources") == src  # a PMC pass of these sources only
     ms_step = elapsed / args.steps * 1e3
     nmsg = int(code.info()["Nmsg"])
     result = {
@@ -201,17 +204,23 @@ def main():
         "roofline": {
             "bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
+            "traffic": pmc.get("hbm_bytes_per_launch") if fresh else None,
+            **({"traffic_over_algorithmic": round(pmc["hbm_bytes_per_launch"] / per[dom], 3)} if fresh else {}),
+            **({"traffic_stale": {"hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch"), "sources": pmc.get("sources"),
+                                  "note": "PMC pass of other sources: not used"}} if pmc is not None and not fresh else {}),
+            "sources": src,
             "algorithmic_bytes_per_launch": per[dom], "avg_launch_ms": round(kinds_rep[dom][0], 5),
             "kernel_ms": {k: round(v[0], 5) for k, v in kinds_rep.items() if v[1]},
             "kernel_ms_event_bracketed": {k: round(v[0], 5) for k, v in kinds.items() if v[1]},
             "amp_launches": {k: v[1] for k, v in kinds.items() if v[1]},
             "eager_amp_decode_ms": round(amp_ms, 3),
         },
-        "bp": {"kernel": "k_bp<sumprod2>", "launch_ms": round(bp_ms, 4), "words": B,
+        "bp": {"kernel": "k_bp<sumprod2> (8 iterations) + k_bp_tail_var / k_bp_tail_chk", "launch_ms": round(bp_ms, 4),
+               "words": B,
                "mean_iterations": round(float(bp_it.mean()), 2), "max_iterations": int(bp_it.max()),
                "edges": nmsg, "edge_updates_per_s": round(float(bp_it.sum()) * nmsg / (bp_ms * 1e-3), 1),
-               "bound": "fp64 VALU (log1p/exp per edge, messages in LDS)"},
+               "bound": "fp64 VALU: the first iterations issue-bound (3 waves per SIMD), the tail one wave per "
+                        "SIMD on the dependent Lxor chain of each check"},
         "errors": {"amp_bits_per_round": r["amp"].sum(axis=0).tolist(),
                    "ldpc_bits_per_round": r["ldpc"].sum(axis=0).tolist(), "bits": int(B * L * 9)},
         "step_share_ms": {k: round(v, 3) for k, v in share.items()},

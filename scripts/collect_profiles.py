@@ -38,7 +38,7 @@ def main():
             subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "graph_trace.py"), tr,
                             os.path.join(dst, f"{RND}_{tag}_graph_trace.txt"), src], check=False,
                            stdout=subprocess.DEVNULL)
-    for tag in ("c2", "c3", "c4", "c3f64", "c3dense"):
+    for tag in ("c2", "c3", "c4", "c3f64", "c3dense", "bp"):
         p = os.path.join(out, f"sq_{tag}.txt")
         if os.path.exists(p):
             shutil.copy(p, os.path.join(dst, f"{RND}_{tag}_sq_counters.txt"))

@@ -304,8 +304,6 @@ struct TailArgs {
   const int* vedge;      // [maxdv][Nv]
   const uint8_t* vdeg;   // [Nv]
   const int* evar;       // [Nmsg] variable node of each edge
-  const int* evd;        // [Nmsg] variable node | its degree << 24 (k_bp_tail_fused)
-  const int4* eadj;      // [Nmsg] that variable's edges in port order, padded with the edge itself
   const int* cstart;     // [Nc+1]
   const int* active;     // [n] words still running
   int* done;             // [B]
@@ -348,76 +346,12 @@ __global__ void __launch_bounds__(256) k_bp_tail_var(TailArgs a) {
   a.app[(size_t)w * a.Nv + j] = aggr;
 }
 
-// Check-regular codes with variable degrees <= 4 (802.16 rate 5/6): the
-// variable update folded into the check kernel, one launch per iteration.  A
-// check thread loads its DC edges' variable tables, then every incoming
-// message of those variables at once (DC x 4 gathers in flight: one wave per
-// SIMD has the registers), and sums ch[v] + the messages in port order for
-// each edge (the adds of k_bp_tail_var, in the same order); the thread of a
-// variable's port-0 edge writes app[v].  One wave per workgroup, S =
-// ceil(Nc / 64) workgroups per word.
-template <int ALGO, int DC>
-__global__ void __launch_bounds__(64) k_bp_tail_fused(TailArgs a) {
-  const int wi = blockIdx.x / a.S, slice = blockIdx.x % a.S;
-  if (wi >= a.n) return;
-  const int w = a.active[wi];
-  if (a.done[w]) return;  // converged in an earlier iteration
-  if (a.lastbad[((a.it - 1) & 1) * a.B + w] != a.it - 1) {
-    // iteration it-1 satisfied every check (c_ldpc.c:196-197): it is the word's last
-    if (slice == 0 && threadIdx.x == 0) {
-      a.iters[w] = a.it - 1;
-      a.done[w] = 1;
-      atomicAdd(a.ndone, 1);
-    }
-    return;
-  }
-  const int c = slice * 64 + (int)threadIdx.x;
-  if (c >= a.Nc) return;
-  const double* rold = a.rold + (size_t)w * a.Nmsg;
-  double* rnew = a.rnew + (size_t)w * a.Nmsg;
-  const double* ch = a.ch + (size_t)w * a.Nv;
-  double* app = a.app + (size_t)w * a.Nv;
-  const int s = c * DC;  // check-regular: cstart[c] = c * DC
-  int vd[DC];
-  int4 adj[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) {
-    vd[k] = a.evd[s + k];
-    adj[k] = a.eadj[s + k];
-  }
-  double x0[DC], x1[DC], x2[DC], x3[DC], cv[DC], r[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) {
-    r[k] = rold[s + k];
-    cv[k] = ch[vd[k] & 0xffffff];
-    x0[k] = rold[adj[k].x];
-    x1[k] = rold[adj[k].y];
-    x2[k] = rold[adj[k].z];
-    x3[k] = rold[adj[k].w];
-  }
-  double l[DC], o[DC];
-#pragma unroll
-  for (int k = 0; k < DC; ++k) {
-    const int d = (int)((unsigned)vd[k] >> 24);
-    double aggr = cv[k];
-    if (0 < d) aggr += x0[k];
-    if (1 < d) aggr += x1[k];
-    if (2 < d) aggr += x2[k];
-    if (3 < d) aggr += x3[k];
-    if (adj[k].x == s + k) app[vd[k] & 0xffffff] = aggr;
-    l[k] = aggr - r[k];
-  }
-  bool bad;
-  if (ALGO == LB_SUMPROD2) {
-    bad = lxfb_fixed_regs<DC, true>(l, o) <= 0.0;
-  } else {
-    bad = lxfb_fixed_regs<DC, false>(l, o) <= 0.0;
-#pragma unroll
-    for (int k = 0; k < DC; ++k) o[k] *= a.corr;
-  }
-#pragma unroll
-  for (int k = 0; k < DC; ++k) rnew[s + k] = o[k];
-  if (bad) a.lastbad[(a.it & 1) * a.B + w] = a.it;
+// the value of the other lane of an even/odd lane pair (DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ double swap_pair(double x) {
+  const unsigned long long u = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, 0xB1, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), 0xB1, 0xF, 0xF, true);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
 constexpr int kTailFixThreads = 256, kTailThreads = 128;
@@ -435,30 +369,55 @@ __global__ void __launch_bounds__(DCFIX > 0 ? kTailFixThreads : kTailThreads) k_
   const int cpw = (a.Nc + a.S - 1) / a.S;
   const int c0 = slice * cpw, c1 = min(a.Nc, c0 + cpw);
   bool anybad = false;
-  for (int c = c0 + (int)threadIdx.x; c < c1; c += blockDim.x) {
-    if constexpr (DCFIX > 0) {
+  if constexpr (DCFIX > 0) {
+    // two lanes per check: lane p = 0 runs the forward chain f, lane p = 1
+    // the backward chain b (its inputs in reverse order), in one instruction
+    // stream; then each takes half of the outputs Lxor(f[k-1], b[k+1]) with
+    // the partner's chain values swapped in (DPP).  The same Lxor calls on
+    // the same operands in the same order as lxfb_fixed_regs: bit-identical.
+    static_assert(DCFIX == 20, "the output split below is written for dc = 20");
+    const int p = threadIdx.x & 1;
+    for (int c = c0 + ((int)threadIdx.x >> 1); c < c1; c += blockDim.x >> 1) {
       const int s = c * DCFIX;  // check-regular: cstart[c] = c * DCFIX
       int ev[DCFIX];
-      double r[DCFIX], l[DCFIX], o[DCFIX];
+      double r[DCFIX], l[DCFIX];
 #pragma unroll
       for (int k = 0; k < DCFIX; ++k) {
-        ev[k] = a.evar[s + k];
-        r[k] = rold[s + k];
+        const int e = s + (p ? DCFIX - 1 - k : k);
+        ev[k] = a.evar[e];
+        r[k] = rold[e];
       }
 #pragma unroll
-      for (int k = 0; k < DCFIX; ++k) l[k] = app[ev[k]] - r[k];
-      bool bad;
-      if (ALGO == LB_SUMPROD2) {
-        bad = lxfb_fixed_regs<DCFIX, true>(l, o) <= 0.0;
-      } else {
-        bad = lxfb_fixed_regs<DCFIX, false>(l, o) <= 0.0;
+      for (int k = 0; k < DCFIX; ++k) l[k] = app[ev[k]] - r[k];  // lane 1: l in reverse order
+      constexpr bool CORR = ALGO == LB_SUMPROD2;
+      double g[DCFIX];  // lane 0: g[i] = f[i]; lane 1: g[i] = b[DC-1-i]
+      g[0] = l[0];
 #pragma unroll
-        for (int k = 0; k < DCFIX; ++k) o[k] *= a.corr;
+      for (int i = 1; i < DCFIX; ++i) g[i] = lxor<CORR>(g[i - 1], l[i]);
+      double pg[9];  // the partner's g[9..17]
+#pragma unroll
+      for (int i = 0; i < 9; ++i) pg[i] = swap_pair(g[9 + i]);
+      double o[10];
+      o[0] = g[18];  // lane 0: o[19] = f[18]; lane 1: o[0] = b[1]
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        // lane 0: k = 1 + i, f[k-1] = g[i], b[k+1] = partner g[17-i]
+        // lane 1: k = 10 + i, f[k-1] = partner g[9+i], b[k+1] = g[8-i]
+        const double fa = p ? pg[i] : g[i];
+        const double bb = p ? g[8 - i] : pg[8 - i];
+        o[1 + i] = lxor<CORR>(fa, bb);
       }
+      if (ALGO != LB_SUMPROD2) {
 #pragma unroll
-      for (int k = 0; k < DCFIX; ++k) rnew[s + k] = o[k];
-      anybad |= bad;
-    } else {
+        for (int i = 0; i < 10; ++i) o[i] *= a.corr;
+      }
+      rnew[s + (p ? 0 : DCFIX - 1)] = o[0];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) rnew[s + (p ? 10 : 1) + i] = o[1 + i];
+      anybad |= p && g[DCFIX - 1] <= 0.0;  // b[0]: lxfb's return value
+    }
+  } else {
+    for (int c = c0 + (int)threadIdx.x; c < c1; c += blockDim.x) {
       const int s = a.cstart[c], dc = a.cstart[c + 1] - s;
       double* L = rows + threadIdx.x * ROW;
       for (int k = 0; k < dc; ++k) L[k] = app[a.evar[s + k]] - rold[s + k];
@@ -558,10 +517,7 @@ struct lb_ctx {
   bool lds = false;
   // tail launches (k_bp_tail): edge tables, per-word state, first tail iteration
   int tail_at = 0, nq = 0, ncu = 256;
-  bool tail_fuse = true;  // k_bp_tail_fused where it applies (LDPC_BP_TAIL_FUSE=0: two kernels)
   int* d_evar = nullptr;
-  int* d_evd = nullptr;   // k_bp_tail_fused tables (variable degrees <= 4)
-  int* d_eadj = nullptr;
   int *d_active = nullptr, *d_nact = nullptr, *d_done = nullptr, *d_lastbad = nullptr;
   int* h_nact = nullptr;  // pinned: [0] words entering the tail, [1..2] done counts of the last chunks
   hipEvent_t evc[2] = {nullptr, nullptr};
@@ -590,8 +546,6 @@ void release(lb_ctx* c) {
   (void)hipFree(c->d_msg);
   (void)hipFree(c->d_it);
   (void)hipFree(c->d_evar);
-  (void)hipFree(c->d_evd);
-  (void)hipFree(c->d_eadj);
   (void)hipFree(c->d_active);
   (void)hipFree(c->d_nact);
   (void)hipFree(c->d_done);
@@ -721,13 +675,14 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   if (n == 0) return LB_OK;
   // m waves per workgroup so that the n words' waves (one thread per check)
   // cover the SIMDs once: S = ceil(Nc / 64m) workgroups per word
-  const long waves = (long)n * ((c->Nc + 63) / 64);
+  // the straight-line check rule runs on lane pairs (32 checks per wave)
+  const bool split = c->fixed && algo != LB_SUMPROD;
+  const long waves = (long)n * ((c->Nc + (split ? 31 : 63)) / (split ? 32 : 64));
   const int mmax = c->fixed && algo != LB_SUMPROD ? kTailFixThreads / 64 : kTailThreads / 64;
-  // check-regular, variable degrees <= 4: one fused launch per iteration, one wave per workgroup
-  const bool fused = c->tail_fuse && c->d_evd && c->fixed && algo != LB_SUMPROD && c->maxdc == 20;
   int m = (int)((waves + 4L * c->ncu - 1) / (4L * c->ncu));
-  m = fused || m < 1 ? 1 : (m > mmax ? mmax : m);
-  const int S = (c->Nc + 64 * m - 1) / (64 * m);
+  m = m < 1 ? 1 : (m > mmax ? mmax : m);
+  const int cpt = split ? 32 : 64;  // checks per wave
+  const int S = (c->Nc + cpt * m - 1) / (cpt * m);
   TailArgs t;
   t.ch = d_ch;
   t.app = d_app;
@@ -735,8 +690,6 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.vedge = c->d_vedge;
   t.vdeg = c->d_vdeg;
   t.evar = c->d_evar;
-  t.evd = c->d_evd;
-  t.eadj = reinterpret_cast<const int4*>(c->d_eadj);
   t.cstart = c->d_cstart;
   t.active = c->d_active;
   t.done = c->d_done;
@@ -750,8 +703,7 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.S = S;
   t.corr = corr;
   double* slot[2] = {c->d_msg, c->d_msg + (size_t)B * c->Nmsg};
-  const TailFn chk = fused ? (algo == LB_SUMPROD2 ? k_bp_tail_fused<LB_SUMPROD2, 20> : k_bp_tail_fused<LB_MINSUM, 20>)
-                           : pick_tail(algo, c->maxdc, c->fixed && algo != LB_SUMPROD);
+  const TailFn chk = pick_tail(algo, c->maxdc, split);
   const TailFn var = pick_tail_var(c->nq);
   const dim3 vgrid((c->Nv + 255) / 256, n);
   // chunks of kTailChunk iterations; after each, the count of words found
@@ -767,7 +719,7 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
       t.rold = slot[(it - c->tail_at) & 1];
       t.rnew = slot[(it - c->tail_at + 1) & 1];
       t.it = it;
-      if (!fused) hipLaunchKernelGGL(var, vgrid, dim3(256), 0, c->stream, t);
+      hipLaunchKernelGGL(var, vgrid, dim3(256), 0, c->stream, t);
       hipLaunchKernelGGL(chk, dim3((unsigned)n * S), dim3(64 * m), 0, c->stream, t);
     }
     HIP_TRY(hipMemcpyAsync(c->h_nact + 1 + (k & 1), c->d_nact + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -891,25 +843,12 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   for (int j = 0; j < Nc; ++j) cs[j + 1] = cs[j] + (int)cdeg[j];
   // tail edge table: the variable node of each edge
   const int nq = maxdv <= 12 ? std::max(1, (maxdv + 3) / 4) : 0;
-  std::vector<int> evar, evd, eadj;
+  std::vector<int> evar;
   if (nq) {
     evar.resize(Nmsg);
     long q = 0;
     for (int j = 0; j < Nv; ++j)
       for (int k = 0; k < vdeg[j]; ++k) evar[intrlv[q++]] = j;
-  }
-  if (nq == 1 && Nv < (1 << 24)) {  // k_bp_tail_fused: per edge its variable (| degree << 24) and that variable's edges
-    evd.resize(Nmsg);
-    eadj.resize((size_t)Nmsg * 4);
-    long q = 0;
-    for (int j = 0; j < Nv; ++j) {
-      for (int k = 0; k < vdeg[j]; ++k) {
-        const int e = (int)intrlv[q + k];
-        evd[e] = j | (int)(vdeg[j] << 24);
-        for (int p = 0; p < 4; ++p) eadj[(size_t)e * 4 + p] = p < vdeg[j] ? (int)intrlv[q + p] : e;
-      }
-      q += vdeg[j];
-    }
   }
 
   lb_ctx* c = new lb_ctx;
@@ -929,8 +868,6 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   if (c->nq) {
     const char* e = getenv("LDPC_BP_TAIL");
     c->tail_at = (e && *e) ? std::max(0, atoi(e)) : kTailAt;
-    const char* f = getenv("LDPC_BP_TAIL_FUSE");
-    c->tail_fuse = !(f && *f == '0');
   }
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };
@@ -939,9 +876,6 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   if ((rc = dev_alloc((void**)&c->d_vdeg, (size_t)Nv))) return bail(rc);
   if ((rc = dev_alloc((void**)&c->d_cstart, (size_t)(Nc + 1) * sizeof(int)))) return bail(rc);
   if (c->nq && (rc = dev_alloc((void**)&c->d_evar, evar.size() * sizeof(int)))) return bail(rc);
-  if (!evd.empty() && ((rc = dev_alloc((void**)&c->d_evd, evd.size() * sizeof(int))) ||
-                       (rc = dev_alloc((void**)&c->d_eadj, eadj.size() * sizeof(int)))))
-    return bail(rc);
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
@@ -955,8 +889,6 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
       hipMemcpyAsync(c->d_vdeg, vd.data(), (size_t)Nv, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(c->d_cstart, cs.data(), (size_t)(Nc + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       (c->nq && hipMemcpyAsync(c->d_evar, evar.data(), evar.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
-      (!evd.empty() && (hipMemcpyAsync(c->d_evd, evd.data(), evd.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-                        hipMemcpyAsync(c->d_eadj, eadj.data(), eadj.size() * sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess)) ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return bail(fail(LB_ERR_HIP, "graph upload failed"));
   *out = c;

@@ -1737,7 +1737,10 @@ __global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real
 // workgroups of a section group are placed on one XCD (blockIdx % 8 labels
 // the XCD) so the group's tables stay in that XCD's L2.
 constexpr int kSG = 16;  // fwd table padding (sections)
-// table bytes of the section groups one XCD works on at a time (SecArgs::gpx)
+// table bytes of the section groups one XCD works on at a time (SecArgs::gpx).
+// C4 binary32 k_secb HBM bytes per launch (PMC, round 4): one pass (6 groups,
+// 4.7 MB) 1.715 GB; 2.5 MB -> 2 x 3 groups 1.495 GB; 1.7 MB -> 3 x 2 groups
+// 1.514 GB; 0.9 MB -> 6 x 1 group 1.711 GB (every pass re-reads z)
 constexpr size_t kSecbL2 = (size_t)5 << 19;  // 2.5 MB of the 4 MB L2
 // sections (waves) per batched workgroup: 8 (two workgroups per CU), or 16
 // (one per CU) where the wider workgroup's LDS holds a larger codeword chunk
@@ -4498,9 +4501,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     // bytes of the XCD's 4 MB L2 (the rest: z chunks, streamed beta)
     const size_t per_group = (size_t)c->WB * ((size_t)c->w + (size_t)n) * 2;
     const int gx = c->Gb / 8 > 0 ? c->Gb / 8 : 1;
-    size_t l2 = kSecbL2;
-    if (const char* e = getenv("SPARC_AMP_SECB_L2_KB")) l2 = (size_t)std::max(1, atoi(e)) << 10;  // measurement only
-    const int fit = (int)std::max<size_t>(1, l2 / per_group);
+    const int fit = (int)std::max<size_t>(1, kSecbL2 / per_group);
     int npass = (gx + fit - 1) / fit;
     c->gpx = (gx + npass - 1) / npass;  // balanced passes
     if (plan & SA_PLAN_ONE_PASS) c->gpx = 1 << 20;

@@ -14,12 +14,16 @@ b() {  # tag, args...
   tail -1 "gpurun_out/bench_$tag.log" > "gpurun_out/bench_$tag.json"
   python3 -c "import json,sys; d=json.load(open('gpurun_out/bench_$tag.json')); r=d['roofline']; print('$tag', d['value'], d['unit'], d['ms_per_step'], 'ms/step', r['kernel'], r['frac'])"
 }
+GROUP=${1:-all}  # a: the factorised-operator lines; b: dense / matrix / joint / rehearsal / sweep
+if [ "$GROUP" != b ]; then
 b c2
 b c3 --workload c3 --no-cpu --no-dense
 b c4 --workload c4 --no-cpu --no-dense
 b c4b1 --workload c4 --batch 1 --no-cpu --no-dense
 b c3f64 --workload c3 --precision fp64 --no-fp64 --no-cpu --no-dense
 b c4f64 --workload c4 --precision fp64 --no-fp64 --no-cpu --no-dense --steps 10 --warmup 2
+fi
+[ "$GROUP" = a ] && exit 0
 b c3dense --workload c3 --backend dense --no-cpu --no-dense --steps 5 --warmup 1
 b c4b1dense --workload c4 --batch 1 --backend dense --no-cpu --no-dense --steps 3 --warmup 1
 b c2matrix --backend matrix --no-cpu --no-dense --no-fp64 --steps 5 --warmup 1
@@ -32,3 +36,6 @@ SPARC_DIST_BACKEND=socket timeout -k 10 400 python -m torch.distributed.run --nn
   > gpurun_out/bench_c2_rehearse_socket2.log 2>&1 || { echo "rehearsal failed"; tail -20 gpurun_out/bench_c2_rehearse_socket2.log; exit 1; }
 grep '^{' gpurun_out/bench_c2_rehearse_socket2.log | tail -1 > gpurun_out/bench_c2_rehearse_socket2.json
 python3 -c "import json; d=json.load(open('gpurun_out/bench_c2_rehearse_socket2.json')); print('rehearsal', d['n_gpus'], d['value'], d['config']['parallelism'])"
+# BASELINE configs[3]: the 10 k-rep L = 768 Monte-Carlo sweep (10 sigma points x 1000 reps, early stop)
+timeout -k 10 300 python scripts/waterfall.py --sweep l768 --reps 1000 --out gpurun_out/waterfall_l768_10k > gpurun_out/waterfall_l768_10k.log 2>&1 || { echo "sweep failed"; tail -5 gpurun_out/waterfall_l768_10k.log; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/waterfall_l768_10k.json')); print('sweep l768 10k reps', round(d['seconds'], 3), 's')"

@@ -29,7 +29,7 @@ def short(name):
         return "k_gemm_f_Ab" if ", 1>" in name else "k_gemm_f_Az"
     for k in ("k_secb", "k_sec2", "k_sec43", "k_sec4", "k_sec8", "k_sec", "k_row2", "k_rowv", "k_rowc", "k_row", "k_dense_az", "k_dense_ab", "k_dense_den", "k_decide",
               "k_gemm_i8", "k_i8_quant", "k_i8_build",
-              "k_bp", "k_llr", "k_bp2sp", "k_sp_norm", "k_colsum"):
+              "k_bp_tail_chk", "k_bp_tail_var", "k_bp_tail_end", "k_bp", "k_llr", "k_bp2sp", "k_sp_norm", "k_colsum"):
         if any(p in name for p in (f"::{k}<", f" {k}<", f" {k}(", f"::{k}(")) or name.startswith((f"{k}<", f"{k}(")):
             return k
     return name.split("(")[0][-40:]

@@ -519,7 +519,9 @@ def main(argv=None, make_op=None):
                               "section_kernel": op64.plan(B)["section_kernel"],
                               "roofline": measure_roofline(op64, args, L, M, n, B, T, "fp64", ms64)}
         del op64
-    if rank == 0 and world == 1 and not args.no_dense:
+    if rank == 0 and not args.no_dense:
+        # after the timed region, on rank 0's GPU: the N-rank line carries the
+        # dense GEMV probe as well
         try:
             result["dense_gemv"] = dense_gemv_probe(device)
         except Exception as e:  # report, never hide

@@ -1,4 +1,4 @@
-"""bench.py's N-rank flow on the CPU: two ranks over the dist module's socket
+"""bench.py's N-rank flow on the CPU: two and four ranks over the dist module's socket
 backend drive bench.main() end to end with a stand-in device operator (the
 bench's own timing, barriers, max-over-ranks, per-rank spread, binary64 leg,
 roofline assembly and the CPU baseline run after the timed region on rank 0).
@@ -70,13 +70,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_rank_bench_line_carries_cpu_baseline_and_spread():
+@pytest.mark.parametrize("world", [2, 4])
+def test_n_rank_bench_line_carries_cpu_baseline_and_spread(world):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    argv = ["--gpus", "2", "--steps", "4", "--warmup", "1", "--no-dense", "--cpu-procs", "1", "--cpu-iters", "1"]
-    ps = [ctx.Process(target=_rank, args=(r, 2, port, q, argv)) for r in range(2)]
+    argv = ["--gpus", str(world), "--steps", "4", "--warmup", "1", "--no-dense", "--cpu-procs", "1", "--cpu-iters", "1"]
+    ps = [ctx.Process(target=_rank, args=(r, world, port, q, argv)) for r in range(world)]
     for p in ps:
         p.start()
     got = dict(q.get(timeout=300) for _ in ps)
@@ -84,11 +85,11 @@ def test_two_rank_bench_line_carries_cpu_baseline_and_spread():
         p.join(timeout=60)
         assert p.exitcode == 0
     line = json.loads(got[0])
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["n_gpus"] == world and line["scaling"] == "weak"
     assert line["value"] > 0 and line["ms_per_step"] > 0
     # per-rank spread of a weak-scaling job
     pr = line["per_rank"]
-    assert 0 < pr["value_min"] <= pr["value_max"] and len(pr["ms_per_step"]) == 2
+    assert 0 < pr["value_min"] <= pr["value_max"] and len(pr["ms_per_step"]) == world
     assert max(pr["ms_per_step"]) <= line["ms_per_step"] + 1e-6  # the line's time is the max over ranks
     # the CPU baseline of an N-rank line, run on rank 0 after the timed region
     cb = line["cpu_baseline"]
@@ -99,5 +100,8 @@ def test_two_rank_bench_line_carries_cpu_baseline_and_spread():
     assert r["kernel"] == "k_sec4" and r["bound"] == "hbm" and 0 < r["frac"] < 1
     assert r["consistency"]["T"] == 64 and r["consistency"]["per_iteration_ms"] > 0
     assert "sources" in r and line["fp64_leg"]["roofline"]["kernel"] == "k_sec4"
-    # rank 1 returns the same line without printing it
-    assert json.loads(got[1])["value"] == line["value"]
+    # the other ranks return the same line without printing it
+    for r in range(1, world):
+        assert json.loads(got[r])["value"] == line["value"]
+    # value = every rank's codewords over the slowest rank's time
+    assert abs(line["value"] - world * pr["value_min"]) <= 1e-3 * line["value"]

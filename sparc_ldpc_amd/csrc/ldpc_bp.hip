@@ -637,7 +637,8 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   if (algo < LB_SUMPROD2 || algo > LB_MINSUM) return fail(LB_ERR_ARG, "unknown decoder type");
   if (max_iter < 0) return fail(LB_ERR_ARG, "max_iter < 0");
   if (B == 0) return LB_OK;
-  const bool tail = c->tail_at > 0 && max_iter > c->tail_at;
+  // the tail's variable kernel puts the words on the grid's y dimension (<= 65535)
+  const bool tail = c->tail_at > 0 && max_iter > c->tail_at && B <= 65535;
   int rc;
   if ((rc = ensure_msg(c, B, tail))) return rc;
   if ((rc = set_attrs(c))) return rc;

@@ -213,3 +213,18 @@ def test_tail_launches_bit_identical(bp, std, rate, z, ebno):
     finally:
         c.set_tail(-1)
     assert c.info()["tail_at"] == 8
+
+
+def test_large_batch_runs_without_the_tail(bp):
+    """More than 65535 words in one call: the decode runs whole in k_bp (the
+    tail's grid has the words on its y dimension), same results as smaller
+    calls for the same words."""
+    c = bp.code("802.16", "1/2", 24)
+    rs = np.random.RandomState(19)
+    X, CH = _awgn(c, rs, 1.6, 8)
+    CH = np.repeat(CH, 8193, axis=0)  # 65544 words
+    A, IT = c.decode_batch(CH, max_iter=20)
+    a8, it8 = c.decode_batch(CH[::8193], max_iter=20)
+    assert np.array_equal(IT[::8193], it8) and np.array_equal(A[::8193], a8)
+    assert np.array_equal(IT.reshape(8, 8193), np.repeat(it8[:, None], 8193, axis=1))
+

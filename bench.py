@@ -49,20 +49,24 @@ def n_of(w):
     return int(w["L"] * np.log2(w["M"]) / w["R"])
 
 
-def synth_y(op, Pl, sigma, seeds):
+def synth_y(op, Pl, sigma, seeds, with_idx=False):
     """Synthetic reps: RandomState(seed) -> L indices in [0, M),
-    then N(0, σ²) noise; x = A β₀ on the device."""
+    then N(0, σ²) noise; x = A β₀ on the device.  with_idx: also the (B, L)
+    transmitted section indices."""
     L, M, n = op.L, op.M, op.n
     c = np.sqrt(n * Pl)
     B = len(seeds)
     beta0 = np.zeros((B, L * M))
     noise = np.empty((B, n))
+    sent = np.empty((B, L), dtype=np.int32)
     for i, s in enumerate(seeds):
         rs = np.random.RandomState(s)
         idx = rs.randint(0, M, L)
+        sent[i] = idx
         beta0[i, np.arange(L) * M + idx] = c
         noise[i] = rs.randn(n) * sigma
-    return op.Ab_batch(beta0) + noise
+    y = op.Ab_batch(beta0) + noise
+    return (y, sent) if with_idx else y
 
 
 def sec_bytes(L, M, n, w, B, G, s, kernel="k_sec4"):
@@ -282,9 +286,10 @@ def load_trace(tag, kernel):
     for line in open(files[-1]):
         if line.startswith("sources sha256 "):
             src = line.split()[-1]
-        m = re.match(r"(\S+)\s+n=\s*(\d+)\s+duration median\s+(\d+) ns.*?(?:exclusive median\s+(\d+) ns)?", line)
+        m = re.match(r"(\S+)\s+n=\s*(\d+)\s+duration median\s+(\d+) ns", line)
         if m and m.group(1) == kernel:
-            hit = (float(m.group(3)), float(m.group(4)) if m.group(4) else None, int(m.group(2)))
+            ex = re.search(r"exclusive median\s+(\d+) ns", line)
+            hit = (float(m.group(3)), float(ex.group(1)) if ex else None, int(m.group(2)))
     if hit is None:
         return None
     return {"duration_ns": hit[0], "exclusive_ns": hit[1], "launches": hit[2], "sources": src,
@@ -304,18 +309,24 @@ def load_pmc(workload, kernel):
 def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
     """Roofline of the dominant kernel of one decode of B codewords.
 
-    `achieved` = algorithmic bytes (ops) per launch / the kernel's mean launch
-    duration measured LIVE here with HIP events on the library's stream: each
-    launch of a short eager decode issued PROFILE_REP times back to back
-    between one event pair (kernel + same-stream boundary, the quantity that
-    adds up to a decode).  Beside it: the committed rocprofv3 graph trace of
-    the same command (`trace`: its exclusive in-graph duration and whether it
-    was taken of these sources), PMC HBM traffic (only when taken of these
-    sources), and a consistency check T x (sum of per-iteration kernel times)
-    <= ms_per_step."""
+    `achieved` = algorithmic bytes (ops) per launch / the kernel's launch
+    duration.  The headline duration is the kernel's in-graph duration: the
+    graph-replay median of the committed rocprofv3 kernel trace of the same
+    command when that profile was taken of these sources (`trace`), else the
+    LIVE dispatch-bound HIP-event time of this run (`dispatch`: an eager decode
+    with every loop kernel launched through hipExtLaunchKernel with a start /
+    stop event pair bound to its own dispatch packet, on the library's stream;
+    the mean over the decode's T launches).  Beside it: the live dispatch
+    figure (`frac_dispatch`), the repeated-launch figure (`frac_events`: each
+    launch issued PROFILE_REP times back to back between one event pair; the
+    repeats re-read inputs their predecessor left in the caches, so this is
+    an optimistic figure), PMC HBM traffic (only when taken of these sources)
+    and a consistency check T x (sum of per-iteration kernel times) <=
+    ms_per_step."""
     from sparc_ldpc_amd._lib import source_hash
     kinds, total_ms = op.profile(B, T, early_stop=False)
     kinds_rep, _ = op.profile(B, min(T, 4), early_stop=False, rep=PROFILE_REP)
+    kinds_disp, disp_total_ms = op.profile(B, T, early_stop=False, rep=0)
     s = 8 if precision == "fp64" else 4
     plan = op.plan(B)
     mfma = plan["section_kernel"] in ("dense_mfma", "matrix_mfma")
@@ -330,13 +341,15 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
     else:
         per = {"k_dense_az": gemv_bytes(L, M, n, s) * B, "k_dense_ab": gemv_bytes(L, M, n, s) * B,
                "k_dense_den": B * (8 * s * L * M + 2 * s * L * M), "k_row": row_bytes(n, B, 8, s)}
-    share = {k: kinds[k][0] * kinds[k][1] for k in per}
+    share = {k: kinds_disp[k][0] * kinds_disp[k][1] for k in per}
     dom = max(share, key=share.get)
-    dom_ms = kinds_rep[dom][0]
     scale = 1e12 if mfma else 1e9
     peak = (F64_PEAK_TFLOPS if precision == "fp64" else F32_PEAK_TFLOPS) if fmfma else (
         I8_PEAK_TOPS if mfma else HBM_PEAK_GBS)
-    achieved = per[dom] / (dom_ms * 1e-3) / scale
+
+    def frac_of(ms):
+        return round(per[dom] / (ms * 1e-3) / scale / peak, 4) if ms and ms > 0 else None
+
     kname = {"k_sec": plan["section_kernel"], "k_row": plan["row_kernel"]}.get(dom, dom)
     if fmfma:
         trace_name = {"k_dense_az": "k_gemm_f_Az", "k_dense_ab": "k_gemm_f_Ab"}[dom]
@@ -349,8 +362,22 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
     else:
         trace_name = kname
     src = source_hash()
-    # consistency: the loop kernels' back-to-back times per iteration, T times
-    per_iter = sum(kinds_rep[k][0] * round(kinds[k][1] / T) for k in kinds if kinds[k][1] >= T)
+    disp_ms = kinds_disp[dom][0]
+    ev_ms = kinds_rep[dom][0]
+    # the trace of the same command, if it was taken of these sources
+    tag = PROFILE_TAGS.get((args.workload, B, op.backend, precision))
+    tr = load_trace(tag, trace_name) if tag else None
+    matched = tr is not None and tr["sources"] == src
+    if matched:
+        dom_ms, timing = tr["duration_ns"] * 1e-6, (
+            f"in-graph duration: graph-replay median of {tr['launches']} launches in {tr['file']} (rocprofv3 "
+            f"kernel trace of this command, taken of these sources {src})")
+    else:
+        dom_ms, timing = disp_ms, ("live: HIP start / stop events bound to each launch's own dispatch "
+                                   "(hipExtLaunchKernel) in an eager decode of this run, mean over its launches")
+    achieved = per[dom] / (dom_ms * 1e-3) / scale
+    # consistency: the loop kernels' dispatch times per iteration, T times
+    per_iter = sum(kinds_disp[k][0] * round(kinds_disp[k][1] / T) for k in kinds_disp if kinds_disp[k][1] >= T)
     roof = {
         "bound": "mfma" if mfma else "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": peak,
         "unit": "TFLOP/s" if mfma else "GB/s", "frac": round(achieved / peak, 4), "traffic": None,
@@ -358,25 +385,31 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
          else "algorithmic_bytes_per_launch"): per[dom],
         **({"ops": ("multiply-adds x 2 (TFLOP/s)" if fmfma else "int8 multiply-adds x 2 (TOP/s)")} if mfma else {}),
         "avg_launch_ms": round(dom_ms, 5),
-        "timing": f"HIP events on the library stream around {PROFILE_REP} back-to-back launches of each kernel "
-                  f"(kernel + same-stream boundary), measured live in this run",
-        "kernel_ms": {k: round(v[0], 5) for k, v in kinds_rep.items() if v[1]},
+        "timing": timing,
+        "frac_dispatch": frac_of(disp_ms),
+        "dispatch_launch_ms": round(disp_ms, 5),
+        "frac_events": frac_of(ev_ms),
+        "events_launch_ms": round(ev_ms, 5),
+        "events_timing": f"repeated-launch timing: HIP events around {PROFILE_REP} back-to-back launches of each "
+                         f"kernel (kernel + same-stream boundary; repeats re-read what their predecessor cached)",
+        "kernel_ms_dispatch": {k: round(v[0], 5) for k, v in kinds_disp.items() if v[1]},
+        "kernel_ms_events": {k: round(v[0], 5) for k, v in kinds_rep.items() if v[1]},
         "kernel_ms_event_bracketed": {k: round(v[0], 5) for k, v in kinds.items() if v[1]},
         "eager_decode_ms": round(total_ms, 3),
         "consistency": {"per_iteration_ms": round(per_iter, 5), "T": T, "T_x_per_iteration_ms": round(T * per_iter, 4),
                         "ms_per_step": ms_per_step, "ok": bool(T * per_iter <= ms_per_step * 1.02)},
         "sources": src,
     }
-    tag = PROFILE_TAGS.get((args.workload, B, op.backend, precision))
-    tr = load_trace(tag, trace_name) if tag else None
     if tr is not None:
-        match = tr["sources"] == src
-        t = {"file": tr["file"], "profile_matches_build": match, "launches": tr["launches"],
-             "in_graph_duration_ms": round(tr["duration_ns"] * 1e-6, 5)}
+        t = {"file": tr["file"], "profile_matches_build": matched, "sources": tr["sources"],
+             "launches": tr["launches"], "in_graph_duration_ms": round(tr["duration_ns"] * 1e-6, 5),
+             "frac_in_graph": frac_of(tr["duration_ns"] * 1e-6)}
         if tr["exclusive_ns"]:
             ex_ms = tr["exclusive_ns"] * 1e-6
             t["exclusive_ms"] = round(ex_ms, 5)
-            t["frac_exclusive"] = round(per[dom] / (ex_ms * 1e-3) / scale / peak, 4)
+            t["frac_exclusive"] = frac_of(ex_ms)
+        if matched:
+            t["live_dispatch_over_trace"] = round(disp_ms / (tr["duration_ns"] * 1e-6), 4)
         roof["trace"] = t
     pmc = load_pmc(f"{args.workload}_{op.backend}_{precision}_B{B}", trace_name)
     if pmc is not None:
@@ -393,21 +426,49 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
     return roof
 
 
-def timed_steps(op, B, T, steps, warmup):
-    """Warmup, then exactly `steps` decodes between barrier + device sync on
-    both sides; returns (this rank's seconds, the max over ranks)."""
+def timed_steps(op, B, T, steps, warmup, sent=None, decide=True):
+    """Warmup, then exactly `steps` decoded steps between barrier + device sync
+    on both sides.  A step is one decode of the staged batch (sa_run, T
+    iterations) plus its decision: the section argmax on the device and the
+    copy of the (B, L) indices into a pinned host slot (sa_decide_async),
+    which the host collects one step behind (sa_decide_collect) while the next
+    decode runs, and scores against the transmitted indices `sent`; the last
+    step's decisions are collected inside the timed region.  decide=False
+    times the decodes alone.  Returns a dict: this rank's seconds, the max
+    over ranks, the timed region's perf_counter stamps and the section errors
+    of the timed steps' decisions."""
     from sparc_ldpc_amd import dist
-    for _ in range(warmup):
-        op.run(B, T, early_stop=False)
+    S = 2
+
+    def run_steps(k0, count, score):
+        errs, decided = 0, 0
+        for k in range(k0, k0 + count):
+            op.run(B, T, early_stop=False)
+            if decide:
+                op.decide_async(B, k % S)
+                if k > k0:
+                    idx = op.decide_collect(B, (k - 1) % S)
+                    if score and sent is not None:
+                        errs += int(np.count_nonzero(idx != sent))
+                    decided += 1
+        if decide and count:
+            idx = op.decide_collect(B, (k0 + count - 1) % S)
+            if score and sent is not None:
+                errs += int(np.count_nonzero(idx != sent))
+            decided += 1
+        return errs, decided
+
+    run_steps(0, warmup, False)
     op.wait()
     dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        op.run(B, T, early_stop=False)
+    errs, decided = run_steps(warmup, steps, True)
     op.wait()
     dist.barrier()
-    mine = time.perf_counter() - t0
-    return mine, float(dist.allreduce_max(np.array([mine]))[0])
+    t1 = time.perf_counter()
+    mine = t1 - t0
+    return {"mine": mine, "elapsed": float(dist.allreduce_max(np.array([mine]))[0]), "t0": t0, "t1": t1,
+            "section_errors": errs, "decided_steps": decided}
 
 
 def parse_args(argv=None):
@@ -471,14 +532,18 @@ def main(argv=None, make_op=None):
                               precision=args.precision, device=device, plan=plan)
     # per-rank synthetic reps: seeds 1000 + rank*B + i (sharded, no overlap)
     seeds = [1000 + rank * B + i for i in range(B)]
-    y = synth_y(op, Pl, sigma, seeds)
+    y, sent = synth_y(op, Pl, sigma, seeds, with_idx=True)
     op.reserve(B, T)
     op.stage(y, Pl)
 
-    mine, elapsed = timed_steps(op, B, T, args.steps, args.warmup)
+    ts = timed_steps(op, B, T, args.steps, args.warmup, sent)
+    mine, elapsed = ts["mine"], ts["elapsed"]
     # every rank's own rate (weak scaling: the spread shows a slow GPU)
     times = dist.allreduce_sum(np.eye(world)[rank] * mine) if world > 1 else np.array([mine])
+    errs = dist.allreduce_sum(np.array([ts["section_errors"], ts["decided_steps"]], dtype=np.float64))
     ms_per_step = round(elapsed / args.steps * 1e3, 4)
+    # the decodes alone (no decision), same protocol: the round-4 definition of a step
+    ts0 = timed_steps(op, B, T, args.steps, min(args.warmup, 1), decide=False)
     roofline = measure_roofline(op, args, L, M, n, B, T, args.precision, ms_per_step)
     result = {
         "metric": f"decoded codewords/sec (T AMP iters) at L={L},M={M}; achieved HBM GB/s vs roofline",
@@ -497,6 +562,14 @@ def main(argv=None, make_op=None):
                    "codewords_per_step_per_gpu": B, "backend": args.backend, "precision": args.precision,
                    "early_stop": False, "parallelism": f"reps sharded over {world} GPU(s)",
                    **({"plan": args.plan} if args.plan else {})},
+        "decisions": {"step": "sa_run (T iterations) + sa_decide_async (section argmax on the device, B x L int32 "
+                              "copied to a pinned host slot) + sa_decide_collect on the host, one step behind the "
+                              "decode in flight; the last step's decisions collected inside the timed region",
+                      "decided_steps": int(errs[1]), "section_errors": int(errs[0]),
+                      "section_error_rate": round(float(errs[0]) / max(1.0, float(errs[1]) * B * L), 8)},
+        "decode_only": {"value": round(B * args.steps * world / ts0["elapsed"], 3),
+                        "ms_per_step": round(ts0["elapsed"] / args.steps * 1e3, 4),
+                        "note": "sa_run alone, beta left on the device (no decision)"},
         "roofline": roofline,
     }
     if world > 1:
@@ -512,10 +585,11 @@ def main(argv=None, make_op=None):
                                  device=device))
         op64.reserve(B, T)
         op64.stage(y, Pl)
-        _, e64 = timed_steps(op64, B, T, args.steps, args.warmup)
+        t64 = timed_steps(op64, B, T, args.steps, args.warmup, sent)
+        e64 = t64["elapsed"]
         ms64 = round(e64 / args.steps * 1e3, 4)
         result["fp64_leg"] = {"value": round(B * args.steps * world / e64, 3), "unit": "codewords/s",
-                              "ms_per_step": ms64, "dtype": "f64",
+                              "ms_per_step": ms64, "dtype": "f64", "section_errors_rank0": t64["section_errors"],
                               "section_kernel": op64.plan(B)["section_kernel"],
                               "roofline": measure_roofline(op64, args, L, M, n, B, T, "fp64", ms64)}
         del op64

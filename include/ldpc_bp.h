@@ -63,8 +63,8 @@ int lb_decode(lb_ctx* ctx, int B, const double* ch, double* app, int* iters, int
               double corr_factor, int max_iter);
 
 /* Device-resident form: d_ch / d_app / d_iters are device pointers on the
- * context's device; runs on the context's stream and returns without waiting
- * (but for the tail's one read-back, see lb_set_tail). */
+ * context's device; queued on the context's stream, returns without waiting
+ * (the tail is sized on the device, see lb_set_tail). */
 int lb_decode_device(lb_ctx* ctx, int B, const double* d_ch, double* d_app, int* d_iters, int algo,
                      double corr_factor, int max_iter);
 
@@ -90,10 +90,13 @@ int lb_info(lb_ctx* ctx, long long* out);
 
 /* Tail launches: a decode runs its first `tail_at` iterations one workgroup
  * per word; the words still running after that are spread over several
- * workgroups each, one launch per iteration (bit-identical results; the run
- * reads back the number of words left once, so lb_decode_device / lb_run
- * wait for the first phase when max_iter > tail_at).  tail_at < 0: the
- * default (8, or the environment's LDPC_BP_TAIL at lb_create); 0: off.
+ * workgroups each, two launches per iteration (bit-identical results).
+ * lb_decode (blocking) reads back the number of words left once and sizes
+ * the tail for them, issuing iterations until a read-back shows every word
+ * done; lb_run / lb_decode_device never wait: every iteration up to
+ * max_iter is queued, sized from the previous tail's word count, and a
+ * launch past the last running word returns at once.  tail_at < 0: the
+ * default chosen at lb_create (8, or the environment's LDPC_BP_TAIL); 0: off.
  * Needs variable degrees <= 12 (LB_ERR_UNSUPPORTED otherwise). */
 int lb_set_tail(lb_ctx* ctx, int tail_at);
 int lb_device_count(void);

@@ -179,11 +179,28 @@ int sa_profile_kinds(void);
  * overhead.  The results left in place are then those of repeated
  * launches (not a decode); re-run sa_run before fetching. */
 int sa_profile_rep(sa_ctx* ctx, int B, int T, int flags, int rep, double* out);
+/* The same eager decode with every loop kernel launched once through
+ * hipExtLaunchKernel with a start / stop event pair bound to the kernel's own
+ * dispatch: {mean ms, launches} per kind is the kernels' execution time in
+ * the decode's order (what a rocprofv3 kernel trace records), with no marker
+ * packets between the launches.  Leaves the decode's results in place. */
+int sa_profile_dispatch(sa_ctx* ctx, int B, int T, int flags, double* out);
 
 /* Per-codeword section decisions (sparc_ldpc.py:452-455: argmax per
  * section, first index on ties) of the last sa_run / sa_amp, computed on
  * device: idx_out is B x L. */
 int sa_decide(sa_ctx* ctx, int B, int32_t* idx_out);
+
+/* The same decision, pipelined: sa_decide_async enqueues the argmax and the
+ * copy of its B x L indices into slot `slot` (0 .. SA_DECIDE_SLOTS-1) of a
+ * context-owned pinned host ring behind the work already on the stream and
+ * returns at once; sa_decide_collect waits for that slot's copy only and
+ * hands its indices to the caller (idx_out: B x L).  A decoder loop queues
+ * decode k + 1 before it collects the decisions of decode k, so the device
+ * never waits on the host. */
+enum { SA_DECIDE_SLOTS = 4 };
+int sa_decide_async(sa_ctx* ctx, int B, int slot);
+int sa_decide_collect(sa_ctx* ctx, int B, int slot, int32_t* idx_out);
 
 /* ---- SPARC <-> LDPC glue of the joint decoder (sparc_ldpc.py:359-712) ---
  * Binary64 kernels on the staged batch; llr / app arrays are [B][ns*log2 M]

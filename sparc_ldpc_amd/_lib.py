@@ -63,7 +63,8 @@ def plan_bits(plan) -> int:
 EXPORTS = (
     "sa_create", "sa_create_ex", "sa_create_matrix", "sa_create_matrix_random", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
     "sa_reserve", "sa_stage", "sa_stage_power_batch", "sa_run", "sa_wait", "sa_fetch", "sa_fetch_z", "sa_run_event_ms",
-    "sa_profile", "sa_profile_rep", "sa_profile_kinds", "sa_decide", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
+    "sa_profile", "sa_profile_rep", "sa_profile_dispatch", "sa_profile_kinds", "sa_decide",
+    "sa_decide_async", "sa_decide_collect", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
     "sa_threshold", "sa_cancel", "sa_plan", "sa_stage_onehot_scaled", "sa_cancel_scaled",
     "sa_host_init", "sa_host_tau", "sa_host_eta", "sa_host_residual",
@@ -92,7 +93,10 @@ _SIG = {
     "sa_run_event_ms": (ct.c_double, [_P]),
     "sa_profile": (_I, [_P, _I, _I, _I, _D]),
     "sa_profile_rep": (_I, [_P, _I, _I, _I, _I, _D]),
+    "sa_profile_dispatch": (_I, [_P, _I, _I, _I, _D]),
     "sa_profile_kinds": (_I, []),
+    "sa_decide_async": (_I, [_P, _I, _I]),
+    "sa_decide_collect": (_I, [_P, _I, _I, ct.POINTER(ct.c_int32)]),
     "sa_decide": (_I, [_P, _I, ct.POINTER(ct.c_int32)]),
     "sa_info": (_I, [_P, ct.POINTER(ct.c_int64)]),
     "sa_device_count": (_I, []),

@@ -295,6 +295,17 @@ __global__ void __launch_bounds__(DCFIX > 0 ? kFixThreads : kMaxThreads) k_bp(Bp
 //     app[v(e)] - r_{t-1}[e] (the reference's extrinsic, the same subtraction)
 //     and the check rule of k_bp.
 // Bit-identical to running the whole decode in k_bp.
+//
+// Two ways to size the tail.  Sized on the host (lb_decode, which blocks
+// anyway): one 4-byte read-back gives the number n of words still running
+// after tail_at iterations, the grids cover exactly those words, and the host
+// stops issuing iterations once a read-back shows every word done.  Sized on
+// the device (lb_run / lb_decode_device, which must not block the caller):
+// every iteration up to max_iter is queued behind the first phase with grids
+// sized from an estimate of n; each kernel reads n and the done count from
+// device memory, strides over the words the estimate did not cover, and
+// returns at once when every word is done.  Same kernels, same arithmetic in
+// the same order: the two are bit-identical.
 struct TailArgs {
   const double* ch;      // [B][Nv]
   double* app;           // [B][Nv]
@@ -307,43 +318,54 @@ struct TailArgs {
   const int* cstart;     // [Nc+1]
   const int* active;     // [n] words still running
   int* done;             // [B]
-  int* ndone;            // [1] words detected as done in the tail (the host's stop test)
+  int* ndone;            // [1] words detected as done in the tail (the stop test)
+  const int* nactive;    // [1] words entering the tail (device-sized mode)
   int* lastbad;          // [2][B]
   int Nv, Nc, Nmsg, B, n, S, it;
+  int dyn;               // 1: n and the stop test from device memory
   double corr;
 };
+
+// words still running in this tail launch; 0 when every word is done
+__device__ __forceinline__ int tail_words(const TailArgs& a) {
+  if (!a.dyn) return a.n;
+  const int n = *a.nactive;
+  return *a.ndone >= n ? 0 : n;
+}
 
 // DV >= the largest variable degree (4, 8 or 12): every port's table entry
 // and message loaded at once, summed in port order with exact selects
 template <int DV>
 __global__ void __launch_bounds__(256) k_bp_tail_var(TailArgs a) {
-  const int wi = blockIdx.y;
-  const int w = a.active[wi];
-  if (a.done[w]) return;  // converged in an earlier iteration
-  if (a.lastbad[((a.it - 1) & 1) * a.B + w] != a.it - 1) {
-    // iteration it-1 satisfied every check (c_ldpc.c:196-197): it is the word's last
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      a.iters[w] = a.it - 1;
-      a.done[w] = 1;
-      atomicAdd(a.ndone, 1);
-    }
-    return;
-  }
+  const int n = tail_words(a);
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= a.Nv) return;
-  const double* rold = a.rold + (size_t)w * a.Nmsg;
-  const int d = a.vdeg[j];
-  int e[DV];
+  for (int wi = blockIdx.y; wi < n; wi += gridDim.y) {
+    const int w = a.active[wi];
+    if (a.done[w]) continue;  // converged in an earlier iteration
+    if (a.lastbad[((a.it - 1) & 1) * a.B + w] != a.it - 1) {
+      // iteration it-1 satisfied every check (c_ldpc.c:196-197): it is the word's last
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.iters[w] = a.it - 1;
+        a.done[w] = 1;
+        atomicAdd(a.ndone, 1);
+      }
+      continue;
+    }
+    if (j >= a.Nv) continue;
+    const double* rold = a.rold + (size_t)w * a.Nmsg;
+    const int d = a.vdeg[j];
+    int e[DV];
 #pragma unroll
-  for (int k = 0; k < DV; ++k) e[k] = a.vedge[(size_t)(k < d ? k : 0) * a.Nv + j];
-  double x[DV];
+    for (int k = 0; k < DV; ++k) e[k] = a.vedge[(size_t)(k < d ? k : 0) * a.Nv + j];
+    double x[DV];
 #pragma unroll
-  for (int k = 0; k < DV; ++k) x[k] = rold[e[k]];
-  double aggr = a.ch[(size_t)w * a.Nv + j];
+    for (int k = 0; k < DV; ++k) x[k] = rold[e[k]];
+    double aggr = a.ch[(size_t)w * a.Nv + j];
 #pragma unroll
-  for (int k = 0; k < DV; ++k)
-    if (k < d) aggr += x[k];
-  a.app[(size_t)w * a.Nv + j] = aggr;
+    for (int k = 0; k < DV; ++k)
+      if (k < d) aggr += x[k];
+    a.app[(size_t)w * a.Nv + j] = aggr;
+  }
 }
 
 // the value of the other lane of an even/odd lane pair (DPP quad_perm [1,0,3,2])
@@ -359,73 +381,75 @@ template <int ALGO, int DCMAX, int DCFIX>
 __global__ void __launch_bounds__(DCFIX > 0 ? kTailFixThreads : kTailThreads) k_bp_tail_chk(TailArgs a) {
   constexpr int ROW = DCMAX + 1;
   __shared__ double rows[DCFIX > 0 ? 1 : kTailThreads * ROW];
-  const int wi = blockIdx.x / a.S, slice = blockIdx.x % a.S;
-  if (wi >= a.n) return;
-  const int w = a.active[wi];
-  if (a.done[w]) return;
-  const double* rold = a.rold + (size_t)w * a.Nmsg;
-  double* rnew = a.rnew + (size_t)w * a.Nmsg;
-  const double* app = a.app + (size_t)w * a.Nv;
+  const int n = tail_words(a);
   const int cpw = (a.Nc + a.S - 1) / a.S;
-  const int c0 = slice * cpw, c1 = min(a.Nc, c0 + cpw);
-  bool anybad = false;
-  if constexpr (DCFIX > 0) {
-    // two lanes per check: lane p = 0 runs the forward chain f, lane p = 1
-    // the backward chain b (its inputs in reverse order), in one instruction
-    // stream; then each takes half of the outputs Lxor(f[k-1], b[k+1]) with
-    // the partner's chain values swapped in (DPP).  The same Lxor calls on
-    // the same operands in the same order as lxfb_fixed_regs: bit-identical.
-    static_assert(DCFIX == 20, "the output split below is written for dc = 20");
-    const int p = threadIdx.x & 1;
-    for (int c = c0 + ((int)threadIdx.x >> 1); c < c1; c += blockDim.x >> 1) {
-      const int s = c * DCFIX;  // check-regular: cstart[c] = c * DCFIX
-      int ev[DCFIX];
-      double r[DCFIX], l[DCFIX];
+  for (int item = blockIdx.x; item < n * a.S; item += gridDim.x) {
+    const int wi = item / a.S, slice = item % a.S;
+    const int w = a.active[wi];
+    if (a.done[w]) continue;
+    const double* rold = a.rold + (size_t)w * a.Nmsg;
+    double* rnew = a.rnew + (size_t)w * a.Nmsg;
+    const double* app = a.app + (size_t)w * a.Nv;
+    const int c0 = slice * cpw, c1 = min(a.Nc, c0 + cpw);
+    bool anybad = false;
+    if constexpr (DCFIX > 0) {
+      // two lanes per check: lane p = 0 runs the forward chain f, lane p = 1
+      // the backward chain b (its inputs in reverse order), in one instruction
+      // stream; then each takes half of the outputs Lxor(f[k-1], b[k+1]) with
+      // the partner's chain values swapped in (DPP).  The same Lxor calls on
+      // the same operands in the same order as lxfb_fixed_regs: bit-identical.
+      static_assert(DCFIX == 20, "the output split below is written for dc = 20");
+      const int p = threadIdx.x & 1;
+      for (int c = c0 + ((int)threadIdx.x >> 1); c < c1; c += blockDim.x >> 1) {
+        const int s = c * DCFIX;  // check-regular: cstart[c] = c * DCFIX
+        int ev[DCFIX];
+        double r[DCFIX], l[DCFIX];
 #pragma unroll
-      for (int k = 0; k < DCFIX; ++k) {
-        const int e = s + (p ? DCFIX - 1 - k : k);
-        ev[k] = a.evar[e];
-        r[k] = rold[e];
+        for (int k = 0; k < DCFIX; ++k) {
+          const int e = s + (p ? DCFIX - 1 - k : k);
+          ev[k] = a.evar[e];
+          r[k] = rold[e];
+        }
+#pragma unroll
+        for (int k = 0; k < DCFIX; ++k) l[k] = app[ev[k]] - r[k];  // lane 1: l in reverse order
+        constexpr bool CORR = ALGO == LB_SUMPROD2;
+        double g[DCFIX];  // lane 0: g[i] = f[i]; lane 1: g[i] = b[DC-1-i]
+        g[0] = l[0];
+#pragma unroll
+        for (int i = 1; i < DCFIX; ++i) g[i] = lxor<CORR>(g[i - 1], l[i]);
+        double pg[9];  // the partner's g[9..17]
+#pragma unroll
+        for (int i = 0; i < 9; ++i) pg[i] = swap_pair(g[9 + i]);
+        double o[10];
+        o[0] = g[18];  // lane 0: o[19] = f[18]; lane 1: o[0] = b[1]
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          // lane 0: k = 1 + i, f[k-1] = g[i], b[k+1] = partner g[17-i]
+          // lane 1: k = 10 + i, f[k-1] = partner g[9+i], b[k+1] = g[8-i]
+          const double fa = p ? pg[i] : g[i];
+          const double bb = p ? g[8 - i] : pg[8 - i];
+          o[1 + i] = lxor<CORR>(fa, bb);
+        }
+        if (ALGO != LB_SUMPROD2) {
+#pragma unroll
+          for (int i = 0; i < 10; ++i) o[i] *= a.corr;
+        }
+        rnew[s + (p ? 0 : DCFIX - 1)] = o[0];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) rnew[s + (p ? 10 : 1) + i] = o[1 + i];
+        anybad |= p && g[DCFIX - 1] <= 0.0;  // b[0]: lxfb's return value
       }
-#pragma unroll
-      for (int k = 0; k < DCFIX; ++k) l[k] = app[ev[k]] - r[k];  // lane 1: l in reverse order
-      constexpr bool CORR = ALGO == LB_SUMPROD2;
-      double g[DCFIX];  // lane 0: g[i] = f[i]; lane 1: g[i] = b[DC-1-i]
-      g[0] = l[0];
-#pragma unroll
-      for (int i = 1; i < DCFIX; ++i) g[i] = lxor<CORR>(g[i - 1], l[i]);
-      double pg[9];  // the partner's g[9..17]
-#pragma unroll
-      for (int i = 0; i < 9; ++i) pg[i] = swap_pair(g[9 + i]);
-      double o[10];
-      o[0] = g[18];  // lane 0: o[19] = f[18]; lane 1: o[0] = b[1]
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        // lane 0: k = 1 + i, f[k-1] = g[i], b[k+1] = partner g[17-i]
-        // lane 1: k = 10 + i, f[k-1] = partner g[9+i], b[k+1] = g[8-i]
-        const double fa = p ? pg[i] : g[i];
-        const double bb = p ? g[8 - i] : pg[8 - i];
-        o[1 + i] = lxor<CORR>(fa, bb);
+    } else {
+      for (int c = c0 + (int)threadIdx.x; c < c1; c += blockDim.x) {
+        const int s = a.cstart[c], dc = a.cstart[c + 1] - s;
+        double* L = rows + threadIdx.x * ROW;
+        for (int k = 0; k < dc; ++k) L[k] = app[a.evar[s + k]] - rold[s + k];
+        anybad |= check_rule<ALGO, DCMAX, 0>(L, dc, a.corr);
+        for (int k = 0; k < dc; ++k) rnew[s + k] = L[k];
       }
-      if (ALGO != LB_SUMPROD2) {
-#pragma unroll
-        for (int i = 0; i < 10; ++i) o[i] *= a.corr;
-      }
-      rnew[s + (p ? 0 : DCFIX - 1)] = o[0];
-#pragma unroll
-      for (int i = 0; i < 9; ++i) rnew[s + (p ? 10 : 1) + i] = o[1 + i];
-      anybad |= p && g[DCFIX - 1] <= 0.0;  // b[0]: lxfb's return value
     }
-  } else {
-    for (int c = c0 + (int)threadIdx.x; c < c1; c += blockDim.x) {
-      const int s = a.cstart[c], dc = a.cstart[c + 1] - s;
-      double* L = rows + threadIdx.x * ROW;
-      for (int k = 0; k < dc; ++k) L[k] = app[a.evar[s + k]] - rold[s + k];
-      anybad |= check_rule<ALGO, DCMAX, 0>(L, dc, a.corr);
-      for (int k = 0; k < dc; ++k) rnew[s + k] = L[k];
-    }
+    if (anybad) a.lastbad[(a.it & 1) * a.B + w] = a.it;
   }
-  if (anybad) a.lastbad[(a.it & 1) * a.B + w] = a.it;
 }
 
 // after the last tail iteration: the iteration count of the words that ran to
@@ -519,9 +543,14 @@ struct lb_ctx {
   int tail_at = 0, nq = 0, ncu = 256;
   int* d_evar = nullptr;
   int *d_active = nullptr, *d_nact = nullptr, *d_done = nullptr, *d_lastbad = nullptr;
-  int* h_nact = nullptr;  // pinned: [0] words entering the tail, [1..2] done counts of the last chunks
+  int* h_nact = nullptr;  // pinned: [0] words entering the tail, [1..2] done counts of the last chunks,
+                        // [3] the last device-sized tail's words
   hipEvent_t evc[2] = {nullptr, nullptr};
+  hipEvent_t evn = nullptr;   // device-sized tails: its word count has landed in h_nact[0]
+  bool est_pending = false;   // a device-sized tail's word count is in flight
+  int est_n = 0, est_B = 0, est_Bq = 0;  // the last landed count and its batch; the batch in flight
   int capTailB = 0;
+  int tail_default = 0;       // tail_at chosen at lb_create (kTailAt or LDPC_BP_TAIL)
   int* d_vedge = nullptr;
   uint8_t* d_vdeg = nullptr;
   int* d_cstart = nullptr;
@@ -553,6 +582,7 @@ void release(lb_ctx* c) {
   if (c->h_nact) (void)hipHostFree(c->h_nact);
   for (hipEvent_t e : c->evc)
     if (e) (void)hipEventDestroy(e);
+  if (c->evn) (void)hipEventDestroy(c->evn);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -609,12 +639,12 @@ int ensure_tail(lb_ctx* c, int B) {
   if ((rc = dev_alloc((void**)&c->d_done, (size_t)B * sizeof(int)))) return rc;
   if ((rc = dev_alloc((void**)&c->d_lastbad, (size_t)2 * B * sizeof(int)))) return rc;
   if (!c->d_nact && (rc = dev_alloc((void**)&c->d_nact, 2 * sizeof(int)))) return rc;
-  for (hipEvent_t& e : c->evc)
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      e = nullptr;
+  for (hipEvent_t* e : {&c->evc[0], &c->evc[1], &c->evn})
+    if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+      *e = nullptr;
       return fail(LB_ERR_HIP, "hipEventCreate failed");
     }
-  if (!c->h_nact && hipHostMalloc((void**)&c->h_nact, 3 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+  if (!c->h_nact && hipHostMalloc((void**)&c->h_nact, 4 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
     c->h_nact = nullptr;
     return fail(LB_ERR_NOMEM, "hipHostMalloc failed");
   }
@@ -632,8 +662,11 @@ int set_attrs(lb_ctx* c) {
   return LB_OK;
 }
 
+// sized_on_host: the tail's shape from the number of words still running
+// (one read-back; the caller blocks anyway), else sized on the device and
+// queued without waiting (see TailArgs)
 int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int algo, double corr,
-           int max_iter) {
+           int max_iter, bool sized_on_host) {
   if (algo < LB_SUMPROD2 || algo > LB_MINSUM) return fail(LB_ERR_ARG, "unknown decoder type");
   if (max_iter < 0) return fail(LB_ERR_ARG, "max_iter < 0");
   if (B == 0) return LB_OK;
@@ -662,23 +695,40 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   a.done = c->d_done;
   a.lastbad = c->d_lastbad;
   a.B = B;
+  // the previous device-sized tail's word count, if it has landed: the estimate
+  // the next device-sized tail's grids are sized for
+  if (c->est_pending && hipEventQuery(c->evn) == hipSuccess) {
+    c->est_n = c->h_nact[3];
+    c->est_B = c->est_Bq;
+    c->est_pending = false;
+  }
   if (tail) HIP_TRY(hipMemsetAsync(c->d_nact, 0, 2 * sizeof(int), c->stream));  // nactive, ndone
   const size_t shm = c->lds ? (size_t)c->Nmsg * sizeof(double) : 0;
   hipLaunchKernelGGL(pick_kernel(algo, c->maxdc, c->lds, c->fixed), dim3(B), dim3(c->nt), shm, c->stream, a);
   HIP_TRY(hipGetLastError());
   if (!tail) return LB_OK;
 
-  // how many words are left decides the tail's shape (one 4-byte read-back)
-  HIP_TRY(hipMemcpyAsync(c->h_nact, c->d_nact, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  const int n = *c->h_nact;
-  if (n < 0 || n > B) return fail(LB_ERR_HIP, "tail word count out of range");
-  if (n == 0) return LB_OK;
-  // m waves per workgroup so that the n words' waves (one thread per check)
+  int n = B;
+  if (sized_on_host) {
+    // how many words are left decides the tail's shape (one 4-byte read-back)
+    HIP_TRY(hipMemcpyAsync(c->h_nact, c->d_nact, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    n = *c->h_nact;
+    if (n < 0 || n > B) return fail(LB_ERR_HIP, "tail word count out of range");
+    if (n == 0) return LB_OK;
+  }
+  // the words the grids are sized for: exact, or the last device-sized tail's
+  // share of its batch applied to this one (a quarter before any), with slack
+  int nsz = n;
+  if (!sized_on_host) {
+    const double share = c->est_B > 0 ? (double)c->est_n / c->est_B : 0.25;
+    nsz = std::min(B, std::max(8, (int)std::ceil(share * B * 1.25)));
+  }
+  // m waves per workgroup so that the words' waves (one thread per check)
   // cover the SIMDs once: S = ceil(Nc / 64m) workgroups per word
   // the straight-line check rule runs on lane pairs (32 checks per wave)
   const bool split = c->fixed && algo != LB_SUMPROD;
-  const long waves = (long)n * ((c->Nc + (split ? 31 : 63)) / (split ? 32 : 64));
+  const long waves = (long)nsz * ((c->Nc + (split ? 31 : 63)) / (split ? 32 : 64));
   const int mmax = c->fixed && algo != LB_SUMPROD ? kTailFixThreads / 64 : kTailThreads / 64;
   int m = (int)((waves + 4L * c->ncu - 1) / (4L * c->ncu));
   m = m < 1 ? 1 : (m > mmax ? mmax : m);
@@ -695,6 +745,7 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.active = c->d_active;
   t.done = c->d_done;
   t.ndone = c->d_nact + 1;
+  t.nactive = c->d_nact;
   t.lastbad = c->d_lastbad;
   t.Nv = c->Nv;
   t.Nc = c->Nc;
@@ -702,31 +753,49 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.B = B;
   t.n = n;
   t.S = S;
+  t.dyn = sized_on_host ? 0 : 1;
   t.corr = corr;
   double* slot[2] = {c->d_msg, c->d_msg + (size_t)B * c->Nmsg};
   const TailFn chk = pick_tail(algo, c->maxdc, split);
   const TailFn var = pick_tail_var(c->nq);
-  const dim3 vgrid((c->Nv + 255) / 256, n);
-  // chunks of kTailChunk iterations; after each, the count of words found
-  // done is copied back, and the host stops issuing chunks once the copy of
-  // two chunks ago shows every word done (the GPU keeps the latest chunk
-  // meanwhile: no stall while words run, no empty launches to max_iter after)
-  for (int it0 = c->tail_at, k = 0; it0 < max_iter; it0 += kTailChunk, ++k) {
-    if (k >= 2) {
-      HIP_TRY(hipEventSynchronize(c->evc[k & 1]));
-      if (c->h_nact[1 + (k & 1)] >= n) break;
-    }
-    for (int it = it0; it < std::min(max_iter, it0 + kTailChunk); ++it) {
+  const dim3 vgrid((c->Nv + 255) / 256, nsz);
+  const dim3 cgrid((unsigned)nsz * S);
+  if (!sized_on_host) {
+    // every iteration queued; a launch past the last running word returns at once
+    for (int it = c->tail_at; it < max_iter; ++it) {
       t.rold = slot[(it - c->tail_at) & 1];
       t.rnew = slot[(it - c->tail_at + 1) & 1];
       t.it = it;
       hipLaunchKernelGGL(var, vgrid, dim3(256), 0, c->stream, t);
-      hipLaunchKernelGGL(chk, dim3((unsigned)n * S), dim3(64 * m), 0, c->stream, t);
+      hipLaunchKernelGGL(chk, cgrid, dim3(64 * m), 0, c->stream, t);
     }
-    HIP_TRY(hipMemcpyAsync(c->h_nact + 1 + (k & 1), c->d_nact + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipEventRecord(c->evc[k & 1], c->stream));
+    // this tail's word count, for the next one's estimate (read when it has landed)
+    HIP_TRY(hipMemcpyAsync(c->h_nact + 3, c->d_nact, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->evn, c->stream));
+    c->est_pending = true;
+    c->est_Bq = B;
+  } else {
+    // chunks of kTailChunk iterations; after each, the count of words found
+    // done is copied back, and the host stops issuing chunks once the copy of
+    // two chunks ago shows every word done (the GPU keeps the latest chunk
+    // meanwhile: no stall while words run, no empty launches to max_iter after)
+    for (int it0 = c->tail_at, k = 0; it0 < max_iter; it0 += kTailChunk, ++k) {
+      if (k >= 2) {
+        HIP_TRY(hipEventSynchronize(c->evc[k & 1]));
+        if (c->h_nact[1 + (k & 1)] >= n) break;
+      }
+      for (int it = it0; it < std::min(max_iter, it0 + kTailChunk); ++it) {
+        t.rold = slot[(it - c->tail_at) & 1];
+        t.rnew = slot[(it - c->tail_at + 1) & 1];
+        t.it = it;
+        hipLaunchKernelGGL(var, vgrid, dim3(256), 0, c->stream, t);
+        hipLaunchKernelGGL(chk, cgrid, dim3(64 * m), 0, c->stream, t);
+      }
+      HIP_TRY(hipMemcpyAsync(c->h_nact + 1 + (k & 1), c->d_nact + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipEventRecord(c->evc[k & 1], c->stream));
+    }
   }
-  hipLaunchKernelGGL(k_bp_tail_end, dim3((n + 255) / 256), dim3(256), 0, c->stream, d_it, c->d_active, c->d_nact,
+  hipLaunchKernelGGL(k_bp_tail_end, dim3((nsz + 255) / 256), dim3(256), 0, c->stream, d_it, c->d_active, c->d_nact,
                      c->d_done, c->d_lastbad, B, max_iter);
   HIP_TRY(hipGetLastError());
   return LB_OK;
@@ -870,6 +939,7 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
     const char* e = getenv("LDPC_BP_TAIL");
     c->tail_at = (e && *e) ? std::max(0, atoi(e)) : kTailAt;
   }
+  c->tail_default = c->tail_at;
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };
   if (hipSetDevice(device) != hipSuccess) return bail(fail(LB_ERR_HIP, "hipSetDevice failed"));
@@ -908,7 +978,7 @@ int lb_decode(lb_ctx* c, int B, const double* ch, double* app, int* iters, int a
   if ((rc = ensure_io(c, B))) return rc;
   const size_t bytes = (size_t)B * c->Nv * sizeof(double);
   HIP_TRY(hipMemcpyAsync(c->d_ch, ch, bytes, hipMemcpyHostToDevice, c->stream));
-  if ((rc = launch(c, B, c->d_ch, c->d_app, c->d_it, algo, corr_factor, max_iter))) return rc;
+  if ((rc = launch(c, B, c->d_ch, c->d_app, c->d_it, algo, corr_factor, max_iter, true))) return rc;
   HIP_TRY(hipMemcpyAsync(app, c->d_app, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(iters, c->d_it, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -920,7 +990,7 @@ int lb_decode_device(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d
   if (!c) return fail(LB_ERR_ARG, "null context");
   if (B < 0 || (B > 0 && (!d_ch || !d_app || !d_iters))) return fail(LB_ERR_ARG, "bad batch arguments");
   HIP_TRY(hipSetDevice(c->dev));
-  return launch(c, B, d_ch, d_app, d_iters, algo, corr_factor, max_iter);
+  return launch(c, B, d_ch, d_app, d_iters, algo, corr_factor, max_iter, false);
 }
 
 int lb_buffers(lb_ctx* c, int B, double** d_ch, double** d_app, int** d_iters) {
@@ -948,7 +1018,7 @@ int lb_run(lb_ctx* c, int B, int algo, double corr_factor, int max_iter) {
   if (!c || B <= 0 || B > c->capB) return fail(LB_ERR_ARG, "run before stage, or B larger than staged");
   HIP_TRY(hipSetDevice(c->dev));
   HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  int rc = launch(c, B, c->d_ch, c->d_app, c->d_it, algo, corr_factor, max_iter);
+  int rc = launch(c, B, c->d_ch, c->d_app, c->d_it, algo, corr_factor, max_iter, false);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c->ev1, c->stream));
   return LB_OK;
@@ -994,7 +1064,7 @@ int lb_info(lb_ctx* c, long long* out) {
 int lb_set_tail(lb_ctx* c, int tail_at) {
   if (!c) return fail(LB_ERR_ARG, "null context");
   if (tail_at > 0 && !c->nq) return fail(LB_ERR_UNSUPPORTED, "tail launches need variable degrees <= 12");
-  c->tail_at = tail_at < 0 ? (c->nq ? kTailAt : 0) : tail_at;
+  c->tail_at = tail_at < 0 ? c->tail_default : tail_at;
   return LB_OK;
 }
 

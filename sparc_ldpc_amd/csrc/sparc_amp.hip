@@ -24,6 +24,7 @@
 // order, so results are bitwise reproducible run to run.
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cfloat>
 #include <cmath>
@@ -43,7 +44,8 @@
 #include "sparc_amp.h"
 
 // 0.3: sa_profile / sa_profile_rep write 2 * sa_profile_kinds() + 1 doubles (13 since 0.2)
-#define SA_VERSION "sparc_amp 0.3 gfx950"
+// 0.4: sa_profile_dispatch (dispatch-bound event pairs), sa_decide_async / sa_decide_collect
+#define SA_VERSION "sparc_amp 0.4 gfx950"
 
 namespace {
 
@@ -3022,20 +3024,37 @@ int ilog2(int x) {
 
 }  // namespace
 
-// Per-launch HIP-event bracketing for sa_profile (eager sequence only).
-// With rep > 1 every bracketed launch is issued rep times back to back
-// between its two events (sa_profile_rep: mean = elapsed / rep), which
-// excludes the event packets' own dispatch overhead from the per-launch time.
+// Per-launch timing for sa_profile (eager sequence only).
+// Event mode: every profiled launch is bracketed by two HIP event records;
+// with rep > 1 it is issued rep times back to back between them
+// (sa_profile_rep: mean = elapsed / rep, which excludes the event packets'
+// own dispatch overhead but lets each repeat re-read what its predecessor
+// left in the caches).  Dispatch mode (sa_profile_dispatch): each launch goes
+// out once through hipExtLaunchKernel with a start / stop event pair that the
+// runtime binds to the kernel's own dispatch packet, so the pair times the
+// kernel's execution in the decode's order (the quantity a rocprofv3 kernel
+// trace records), with no marker packets in the stream.
 struct Prof {
   std::vector<std::tuple<int, hipEvent_t, hipEvent_t>> ev;
   int rep = 1;
-  int begin(hipStream_t s, int kind) {
+  bool dispatch = false;
+  int kind = 0;
+  int begin(hipStream_t s, int k) {
+    kind = k;
+    if (dispatch) return 0;
     hipEvent_t a = nullptr, b = nullptr;
-    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
-    ev.emplace_back(kind, a, b);
+    if (add(&a, &b)) return -1;
     return hipEventRecord(a, s) == hipSuccess ? 0 : -1;
   }
-  void end(hipStream_t s) { (void)hipEventRecord(std::get<2>(ev.back()), s); }
+  void end(hipStream_t s) {
+    if (!dispatch) (void)hipEventRecord(std::get<2>(ev.back()), s);
+  }
+  int add(hipEvent_t* a, hipEvent_t* b) {
+    *a = *b = nullptr;
+    if (hipEventCreate(a) != hipSuccess || hipEventCreate(b) != hipSuccess) return -1;
+    ev.emplace_back(kind, *a, *b);
+    return 0;
+  }
   ~Prof() {
     for (auto& e : ev) {
       (void)hipEventDestroy(std::get<1>(e));
@@ -3046,7 +3065,10 @@ struct Prof {
 
 enum { K_SEC = 0, K_ROW = 1, K_DAZ = 2, K_DDEN = 3, K_DAB = 4, K_QNT = 5, K_NKINDS = 6 };
 
-#define PROF_REPS(c) for (int _rep = 0, _nrep = (c)->prof ? (c)->prof->rep : 1; _rep < _nrep; ++_rep)
+// Launch of a loop kernel on the context's stream, timed as sa_profile asks
+// (plain launch when no profile is running).
+template <typename F, typename... Args>
+void plaunch(sa_ctx* c, F kernel, dim3 grid, dim3 block, size_t lds, Args... args);
 
 struct sa_ctx {
   Prof* prof = nullptr;
@@ -3124,7 +3146,25 @@ struct sa_ctx {
   size_t bytes = 0;
   std::map<std::tuple<int, int, int, int>, hipGraphExec_t> graphs;
   int last_B = 0, last_T = 0;
+  // pinned ring of sa_decide_async: SA_DECIDE_SLOTS slots of dec_cap indices
+  int32_t* h_dec = nullptr;
+  size_t dec_cap = 0;
+  hipEvent_t dec_ev[SA_DECIDE_SLOTS] = {};
+  int dec_B[SA_DECIDE_SLOTS] = {};
 };
+
+template <typename F, typename... Args>
+void plaunch(sa_ctx* c, F kernel, dim3 grid, dim3 block, size_t lds, Args... args) {
+  if (c->prof && c->prof->dispatch) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (c->prof->add(&a, &b) == 0) {
+      hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, c->stream, a, b, 0u, args...);
+      return;
+    }
+  }
+  const int nrep = c->prof ? c->prof->rep : 1;
+  for (int r = 0; r < nrep; ++r) kernel<<<grid, block, lds, c->stream>>>(args...);
+}
 
 namespace {
 
@@ -3392,7 +3432,7 @@ void launch_sec_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.RS = row_splits(c, B);
   dim3 grid(c->G * a.RS, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
-  PROF_REPS(c) k_sec<real, E><<<grid, 256, c->sec_lds, c->stream>>>(a);
+  plaunch(c, k_sec<real, E>, grid, 256, c->sec_lds, a);
   if (c->prof) c->prof->end(c->stream);
 }
 
@@ -3412,17 +3452,17 @@ void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
   if constexpr (CB * sizeof(real) == 16) {
     if (a.zil) {
       if (c->WB == kWB16)
-        PROF_REPS(c) k_secb<real, E, CB, kWB16, true><<<grid, kWB16 * 64, c->secb_lds, c->stream>>>(a);
+        plaunch(c, k_secb<real, E, CB, kWB16, true>, grid, kWB16 * 64, c->secb_lds, a);
       else
-        PROF_REPS(c) k_secb<real, E, CB, kWB, true><<<grid, kWB * 64, c->secb_lds, c->stream>>>(a);
+        plaunch(c, k_secb<real, E, CB, kWB, true>, grid, kWB * 64, c->secb_lds, a);
       done = true;
     }
   }
   if (!done) {
     if (c->WB == kWB16)
-      PROF_REPS(c) k_secb<real, E, CB, kWB16><<<grid, kWB16 * 64, c->secb_lds, c->stream>>>(a);
+      plaunch(c, k_secb<real, E, CB, kWB16>, grid, kWB16 * 64, c->secb_lds, a);
     else
-      PROF_REPS(c) k_secb<real, E, CB, kWB><<<grid, kWB * 64, c->secb_lds, c->stream>>>(a);
+      plaunch(c, k_secb<real, E, CB, kWB>, grid, kWB * 64, c->secb_lds, a);
   }
   if (c->prof) c->prof->end(c->stream);
 }
@@ -3481,8 +3521,8 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout, int pt =
   if (c->prof) c->prof->begin(c->stream, K_SEC);
   if (c->sec3) {
     switch (c->M / 256) {
-      case 1: PROF_REPS(c) k_sec43<real, 1><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
-      case 2: PROF_REPS(c) k_sec43<real, 2><<<grid, 768, c->sec3_lds, c->stream>>>(a); break;
+      case 1: plaunch(c, k_sec43<real, 1>, grid, 768, c->sec3_lds, a); break;
+      case 2: plaunch(c, k_sec43<real, 2>, grid, 768, c->sec3_lds, a); break;
       default: return fail(SA_ERR_UNSUPPORTED, "k_sec43: M");
     }
     if (c->prof) c->prof->end(c->stream);
@@ -3491,11 +3531,11 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout, int pt =
   }
   if (c->sec4) {
     switch (c->M / 256) {
-      case 1: PROF_REPS(c) k_sec4<real, 1><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 2: PROF_REPS(c) k_sec4<real, 2><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 4: PROF_REPS(c) k_sec4<real, 4><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 8: PROF_REPS(c) k_sec4<real, 8><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
-      case 16: PROF_REPS(c) k_sec4<real, 16><<<grid, 512, c->sec4_lds, c->stream>>>(a); break;
+      case 1: plaunch(c, k_sec4<real, 1>, grid, 512, c->sec4_lds, a); break;
+      case 2: plaunch(c, k_sec4<real, 2>, grid, 512, c->sec4_lds, a); break;
+      case 4: plaunch(c, k_sec4<real, 4>, grid, 512, c->sec4_lds, a); break;
+      case 8: plaunch(c, k_sec4<real, 8>, grid, 512, c->sec4_lds, a); break;
+      case 16: plaunch(c, k_sec4<real, 16>, grid, 512, c->sec4_lds, a); break;
       default: return fail(SA_ERR_UNSUPPORTED, "k_sec4: M");
     }
     if (c->prof) c->prof->end(c->stream);
@@ -3503,12 +3543,12 @@ int launch_sec2(sa_ctx* c, int B, int t, int es, void* bin, void* bout, int pt =
     return SA_OK;
   }
   switch (c->M / 128) {
-    case 1: PROF_REPS(c) k_sec2<real, 1><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 2: PROF_REPS(c) k_sec2<real, 2><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 4: PROF_REPS(c) k_sec2<real, 4><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 8: PROF_REPS(c) k_sec2<real, 8><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 16: PROF_REPS(c) k_sec2<real, 16><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
-    case 32: PROF_REPS(c) k_sec2<real, 32><<<grid, 256, c->sec2_lds, c->stream>>>(a); break;
+    case 1: plaunch(c, k_sec2<real, 1>, grid, 256, c->sec2_lds, a); break;
+    case 2: plaunch(c, k_sec2<real, 2>, grid, 256, c->sec2_lds, a); break;
+    case 4: plaunch(c, k_sec2<real, 4>, grid, 256, c->sec2_lds, a); break;
+    case 8: plaunch(c, k_sec2<real, 8>, grid, 256, c->sec2_lds, a); break;
+    case 16: plaunch(c, k_sec2<real, 16>, grid, 256, c->sec2_lds, a); break;
+    case 32: plaunch(c, k_sec2<real, 32>, grid, 256, c->sec2_lds, a); break;
     default: return fail(SA_ERR_UNSUPPORTED, "k_sec2: M");
   }
   if (c->prof) c->prof->end(c->stream);
@@ -3591,24 +3631,24 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt 
   if (c->row_kind == 5 && mode != ROW_ABOUT) {
     constexpr int CBz = 16 / (int)sizeof(real);  // codewords per 16-byte row
     a.Bc = B;
-    PROF_REPS(c) k_rowc<real, CBz><<<dim3(c->NZ2, (B + CBz - 1) / CBz), 256, 0, c->stream>>>(a, mode == ROW_AMP ? 1 : 0);
+    plaunch(c, k_rowc<real, CBz>, dim3(c->NZ2, (B + CBz - 1) / CBz), 256, 0, a, mode == ROW_AMP ? 1 : 0);
   } else if (c->row_kind == 5) {  // A beta out of k_sec's [B][G][n] partials (sa_Ab after a batched decode)
-    PROF_REPS(c) k_row<real, 4><<<dim3(c->NZ, B), 4 * 64, 0, c->stream>>>(a);
+    plaunch(c, k_row<real, 4>, dim3(c->NZ, B), 4 * 64, 0, a);
   } else if (c->row_kind == 1) {
-    PROF_REPS(c) k_row2<real><<<dim3(c->NZ16, B), 512, 0, c->stream>>>(a);
+    plaunch(c, k_row2<real>, dim3(c->NZ16, B), 512, 0, a);
   } else if (c->row_kind == 4) {
-    PROF_REPS(c) k_row2<real, 16><<<dim3(c->NZh, B), 512, 0, c->stream>>>(a);
+    plaunch(c, k_row2<real, 16>, dim3(c->NZh, B), 512, 0, a);
   } else if (c->row_kind == 2) {
     constexpr int V = 16 / (int)sizeof(real);  // 16-byte rows
-    PROF_REPS(c) k_rowv<real, V><<<dim3(c->nz_cur, B), 256, 0, c->stream>>>(a);
+    plaunch(c, k_rowv<real, V>, dim3(c->nz_cur, B), 256, 0, a);
   } else if (c->row_kind == 3) {
     if constexpr (sizeof(real) == 4) {
-      PROF_REPS(c) k_rowv<float, 2><<<dim3(c->NZ2, B), 256, 0, c->stream>>>(a);
+      plaunch(c, k_rowv<float, 2>, dim3(c->NZ2, B), 256, 0, a);
     } else {
       return SA_ERR_UNSUPPORTED;  // never chosen for binary64 (row_kind_for)
     }
   } else {
-    PROF_REPS(c) k_row<real, 4><<<dim3(c->NZ, B), 4 * 64, 0, c->stream>>>(a);
+    plaunch(c, k_row<real, 4>, dim3(c->NZ, B), 4 * 64, 0, a);
   }
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
@@ -3631,7 +3671,7 @@ int launch_dense_az(sa_ctx* c, int B, int t, int es, int mode) {
   DenseArgs<real> a = dense_args<real>(c, t, es, mode);
   dim3 grid((unsigned)((c->lda / V16<real>::N + 255) / 256), c->RS, B);
   if (c->prof) c->prof->begin(c->stream, K_DAZ);
-  PROF_REPS(c) k_dense_az<real><<<grid, 256, 0, c->stream>>>(a);
+  plaunch(c, k_dense_az<real>, grid, 256, 0, a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -3642,7 +3682,7 @@ int launch_dense_ab(sa_ctx* c, int B, int t, int es, int mode) {
   DenseArgs<real> a = dense_args<real>(c, t, es, mode);
   dim3 grid((unsigned)((c->n + kDenseRows - 1) / kDenseRows), c->KS, B);
   if (c->prof) c->prof->begin(c->stream, K_DAB);
-  PROF_REPS(c) k_dense_ab<real><<<grid, 256, 0, c->stream>>>(a, (const real*)c->d_tau);
+  plaunch(c, k_dense_ab<real>, grid, 256, 0, a, (const real*)c->d_tau);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -3652,7 +3692,7 @@ template <typename real, int E>
 void launch_dense_den_e(sa_ctx* c, int B, const DenArgs<real>& a, bool i8) {
   dim3 grid(c->Gd, B);
   if (c->prof) c->prof->begin(c->stream, K_DDEN);
-  PROF_REPS(c) k_dense_den<real, E><<<grid, 256, 0, c->stream>>>(a, (const real*)c->d_c, (real*)c->d_beta,
+  plaunch(c, k_dense_den<real, E>, grid, 256, 0, a, (const real*)c->d_c, (real*)c->d_beta,
                                                (real*)c->d_bbp, (real*)c->d_tau, c->d_iters, c->Gd,
                                                i8 ? c->d_bq : nullptr, (long long)c->Bp8 * c->LMp8,
                                                c->LMp8, c->d_bfix);
@@ -3688,7 +3728,7 @@ int launch_dense_den(sa_ctx* c, int B, int t, int es, bool i8 = false, bool one_
 template <int NP>
 int launch_i8_quant(sa_ctx* c, int B, const void* src, long long ld, int len, int8_t* q, long long K, double* sc) {
   if (c->prof) c->prof->begin(c->stream, K_QNT);
-  PROF_REPS(c) k_i8_quant<NP><<<B, 256, 0, c->stream>>>((const float*)src, ld, len, q, (long long)c->Bp8 * K, K,
+  plaunch(c, k_i8_quant<NP>, B, 256, 0, (const float*)src, ld, len, q, (long long)c->Bp8 * K, K,
                                                          sc, 1.0 / std::sqrt((double)c->n));
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
@@ -3711,7 +3751,7 @@ int launch_gemm_i8(sa_ctx* c, int B, const int8_t* X, long long K, const int8_t*
   const long long grid = (long long)a.XT * a.YT * S;
   if (grid > 0x7fffffff) return fail(SA_ERR_UNSUPPORTED, "k_gemm_i8: grid too large");
   if (c->prof) c->prof->begin(c->stream, kind);
-  PROF_REPS(c) k_gemm_i8<NP><<<(unsigned)grid, 512, I8Tile<NP>::Lds, c->stream>>>(a);
+  plaunch(c, k_gemm_i8<NP>, (unsigned)grid, 512, I8Tile<NP>::Lds, a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -3799,9 +3839,9 @@ int launch_gemm_f(sa_ctx* c, int B, const real* X, long long ldx, const real* Y,
   if (grid > 0x7fffffff) return fail(SA_ERR_UNSUPPORTED, "k_gemm_f: grid too large");
   if (c->prof) c->prof->begin(c->stream, kind);
   if (kind == K_DAB)
-    PROF_REPS(c) k_gemm_f<real, 1><<<(unsigned)grid, 512, kFLds, c->stream>>>(a);
+    plaunch(c, k_gemm_f<real, 1>, (unsigned)grid, 512, kFLds, a);
   else
-    PROF_REPS(c) k_gemm_f<real, 0><<<(unsigned)grid, 512, kFLds, c->stream>>>(a);
+    plaunch(c, k_gemm_f<real, 0>, (unsigned)grid, 512, kFLds, a);
   if (c->prof) c->prof->end(c->stream);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -4916,6 +4956,9 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_stage);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (auto& e : c->dec_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->h_dec) (void)hipHostFree(c->h_dec);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -5147,7 +5190,9 @@ int sa_profile(sa_ctx* c, int B, int T, int flags, double* out) { return sa_prof
 
 int sa_profile_kinds(void) { return K_NKINDS; }
 
-int sa_profile_rep(sa_ctx* c, int B, int T, int flags, int rep, double* out) {
+extern "C++" {
+namespace {
+int profile_impl(sa_ctx* c, int B, int T, int flags, int rep, bool dispatch, double* out) {
   if (int rc0 = check_op(c, "sa_profile")) return rc0;
   if (B <= 0 || T <= 0 || !out || B > c->Bcap || T > c->Tcap || !c->power_set || rep < 1 || rep > 1024)
     return fail(SA_ERR_ARG, "sa_profile: bad arguments (reserve and stage first)");
@@ -5158,6 +5203,7 @@ int sa_profile_rep(sa_ctx* c, int B, int T, int flags, int rep, double* out) {
     if (int rci = ensure_invb(c)) return rci;
   Prof prof;
   prof.rep = rep;
+  prof.dispatch = dispatch;
   c->prof = &prof;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   HIP_TRY(hipEventCreate(&e0));
@@ -5191,11 +5237,20 @@ int sa_profile_rep(sa_ctx* c, int B, int T, int flags, int rep, double* out) {
   (void)hipEventDestroy(e1);
   return rc;
 }
+}  // namespace
+}  // extern "C++"
 
-int sa_decide(sa_ctx* c, int B, int32_t* idx_out) {
-  if (check_ctx(c)) return SA_ERR_ARG;
-  if (B <= 0 || B > c->Bcap || !idx_out) return fail(SA_ERR_ARG, "sa_decide: bad arguments");
-  HIP_TRY(hipSetDevice(c->device));
+int sa_profile_rep(sa_ctx* c, int B, int T, int flags, int rep, double* out) {
+  return profile_impl(c, B, T, flags, rep, false, out);
+}
+
+int sa_profile_dispatch(sa_ctx* c, int B, int T, int flags, double* out) {
+  return profile_impl(c, B, T, flags, 1, true, out);
+}
+
+extern "C++" {
+namespace {
+int launch_decide(sa_ctx* c, int B) {
   dim3 grid((c->L + 3) / 4, B);
 #define SA_DEC(EE)                                                                                             \
   case EE:                                                                                                     \
@@ -5207,11 +5262,59 @@ int sa_decide(sa_ctx* c, int B, int32_t* idx_out) {
   switch (c->E) { SA_DEC(1) SA_DEC(2) SA_DEC(4) SA_DEC(8) SA_DEC(16) SA_DEC(32) SA_DEC(64) }
 #undef SA_DEC
   HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+}  // namespace
+}  // extern "C++"
+
+int sa_decide(sa_ctx* c, int B, int32_t* idx_out) {
+  if (check_ctx(c)) return SA_ERR_ARG;
+  if (B <= 0 || B > c->Bcap || !idx_out) return fail(SA_ERR_ARG, "sa_decide: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  if (int rc = launch_decide(c, B)) return rc;
   HIP_TRY(hipMemcpyAsync(idx_out, c->d_idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
 
+int sa_decide_async(sa_ctx* c, int B, int slot) {
+  if (check_ctx(c)) return SA_ERR_ARG;
+  if (B <= 0 || B > c->Bcap || slot < 0 || slot >= SA_DECIDE_SLOTS)
+    return fail(SA_ERR_ARG, "sa_decide_async: bad arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t per = (size_t)c->Bcap * c->L;  // one slot holds a whole staged batch
+  if (!c->h_dec || c->dec_cap < per) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->h_dec) (void)hipHostFree(c->h_dec);
+    c->h_dec = nullptr;
+    c->dec_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&c->h_dec, per * SA_DECIDE_SLOTS * sizeof(int32_t), hipHostMallocDefault));
+    c->dec_cap = per;
+    for (int k = 0; k < SA_DECIDE_SLOTS; ++k) {
+      if (!c->dec_ev[k]) HIP_TRY(hipEventCreateWithFlags(&c->dec_ev[k], hipEventDisableTiming));
+      c->dec_B[k] = 0;
+    }
+  }
+  // the slot's previous indices must have left the ring before they are overwritten
+  // (the stream is in order: the copy below cannot overtake it anyway)
+  if (int rc = launch_decide(c, B)) return rc;
+  int32_t* dst = c->h_dec + (size_t)slot * c->dec_cap;
+  HIP_TRY(hipMemcpyAsync(dst, c->d_idx, (size_t)B * c->L * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(c->dec_ev[slot], c->stream));
+  c->dec_B[slot] = B;
+  return SA_OK;
+}
+
+int sa_decide_collect(sa_ctx* c, int B, int slot, int32_t* idx_out) {
+  if (check_ctx(c)) return SA_ERR_ARG;
+  if (slot < 0 || slot >= SA_DECIDE_SLOTS || !idx_out || !c->h_dec || c->dec_B[slot] != B || B <= 0)
+    return fail(SA_ERR_ARG, "sa_decide_collect: no decision of this batch queued in the slot");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->dec_ev[slot]));
+  std::memcpy(idx_out, c->h_dec + (size_t)slot * c->dec_cap, (size_t)B * c->L * sizeof(int32_t));
+  c->dec_B[slot] = 0;
+  return SA_OK;
+}
 
 int sa_encode(sa_ctx* c, int B, const int32_t* idx, const double* noise) {
   if (check_ctx(c)) return SA_ERR_ARG;

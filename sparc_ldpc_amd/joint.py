@@ -38,7 +38,7 @@ from . import ldpc as _ldpc
 from .harness import SPARCParams, LDPCParams, pa_parameterised, ebno_to_sigma
 from .operators import SparcOperator, make_ordering
 
-__all__ = ["JointDecoder", "joint_decoder", "draw_reps", "amp_ldpc_sim_ldpc", "soft_amp_ldpc_sim",
+__all__ = ["JointDecoder", "JointPipeline", "joint_decoder", "draw_reps", "amp_ldpc_sim_ldpc", "soft_amp_ldpc_sim",
            "hardinitbeta_amp_ldpc_sim", "sim_ldpc", "waterfall", "soft_hard_plot", "sp2bp", "bp2sp", "mc_joint"]
 
 MODES = ("originalHard", "soft", "hard", "threshold")
@@ -275,7 +275,76 @@ class JointDecoder:
         return _popcount(np.bitwise_xor(np.asarray(a, np.int64), np.asarray(b, np.int64))).sum(axis=1)
 
 
+class JointPipeline:
+    """A batch of the joint decoder cut into `parts` consecutive slices, each
+    decoded by its own JointDecoder (its own operator context and HIP stream,
+    its own LDPC context and stream) from its own host thread, so that one
+    slice's belief-propagation tail (a few words on a few CUs for up to
+    MAX_ITCOUNT iterations, c_ldpc.c:7) runs beside another slice's AMP
+    kernels instead of in front of them.  The library calls release the GIL;
+    every slice's steps stay in the reference's order on its own streams, and
+    a codeword's decode does not depend on the batch it is in, so the per-rep
+    results are those of one JointDecoder over the whole batch
+    (tests/test_gpu_joint.py)."""
+
+    def __init__(self, jd: JointDecoder, parts=2):
+        from concurrent.futures import ThreadPoolExecutor
+        self.jd = jd
+        self.parts = [jd]
+        op, code = jd.op, jd.code
+        for _ in range(int(parts) - 1):
+            c2 = _ldpc.code(code.standard, code.rate, code.z, code.ptype, device=code._device)
+            self.parts.append(JointDecoder(jd.L, jd.M, jd.n, c2, jd.T, op.backend, op.precision, op.device))
+        self._pool = ThreadPoolExecutor(max_workers=len(self.parts), thread_name_prefix="joint")
+        self._slices = None
+
+    def _cut(self, B):
+        k = len(self.parts)
+        edges = [B * i // k for i in range(k + 1)]
+        return [slice(edges[i], edges[i + 1]) for i in range(k) if edges[i + 1] > edges[i]]
+
+    def _map(self, fn):
+        futs = [self._pool.submit(fn, part, sl) for part, sl in zip(self.parts, self._slices)]
+        return [f.result() for f in futs]
+
+    def stage(self, idx, noise, Pl):
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        noise = np.asarray(noise, dtype=np.float64).reshape(idx.shape[0], -1)
+        self._slices = self._cut(idx.shape[0])
+        self._map(lambda part, sl: part.stage(idx[sl], noise[sl], Pl))
+
+    def decode_staged(self, idx, Pl, mode="soft", soft_iter=2, threshold=0.5, unit_cancel=False):
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        assert self._slices is not None and self._slices[-1].stop == idx.shape[0], "stage the batch first"
+        outs = self._map(lambda part, sl: part.decode_staged(idx[sl], Pl, mode, soft_iter, threshold, unit_cancel))
+        return {k: np.concatenate([o[k] for o in outs], axis=0) for k in outs[0]}
+
+    def run(self, idx, noise, Pl, mode="soft", soft_iter=2, threshold=0.5, unit_cancel=False):
+        self.stage(idx, noise, Pl)
+        return self.decode_staged(idx, Pl, mode, soft_iter, threshold, unit_cancel)
+
+    def wait(self):
+        for part in self.parts:
+            part.op.wait()
+
+    def close(self):
+        self._pool.shutdown(wait=True)
+
+
 _JD_CACHE: "OrderedDict[tuple, JointDecoder]" = OrderedDict()
+_JP_CACHE: "dict[int, JointPipeline]" = {}
+
+# batches of at least this many codewords are decoded as two concurrent halves
+PIPELINE_MIN_BATCH = 64
+
+
+def joint_pipeline(jd: JointDecoder, parts=2) -> JointPipeline:
+    """The cached JointPipeline over jd (the extra slices' tables built once)."""
+    jp = _JP_CACHE.get(id(jd))
+    if jp is None or jp.jd is not jd or len(jp.parts) != parts:
+        jp = JointPipeline(jd, parts)
+        _JP_CACHE[id(jd)] = jp
+    return jp
 
 
 def joint_decoder(L, M, n, ldpcparams: LDPCParams, T, backend=None, precision=None, device=None):
@@ -343,15 +412,21 @@ def hardinitbeta_amp_ldpc_sim(sparcparams: SPARCParams, ldpcparams: LDPCParams, 
     return [float(e) / tb for e in r["amp"][0]], [float(e) / tb for e in r["ldpc"][0]], jd.R
 
 
-def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256, threshold=0.5, unit_cancel=False):
+def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256, threshold=0.5, unit_cancel=False,
+             pipeline=None):
     """Seeded batched reps: rep s draws from RandomState(s) in the reference's
-    order.  Returns the per-rep error-count dict of JointDecoder.run, in seed order."""
+    order.  Returns the per-rep error-count dict of JointDecoder.run, in seed
+    order.  pipeline (default: batches of PIPELINE_MIN_BATCH or more in the
+    soft / hard / originalHard modes): decode each batch as two concurrent
+    halves (JointPipeline), with the same per-rep results."""
     seeds = list(seeds)
     parts = []
     for s0 in range(0, len(seeds), batch):
         chunk = seeds[s0:s0 + batch]
         idx, noise = jd.draw([np.random.RandomState(s) for s in chunk], len(chunk), sigma)
-        parts.append(jd.run(idx, noise, Pl, mode, soft_iter, threshold, unit_cancel))
+        pipe = pipeline if pipeline is not None else (len(chunk) >= PIPELINE_MIN_BATCH and mode != "threshold")
+        runner = joint_pipeline(jd) if pipe else jd
+        parts.append(runner.run(idx, noise, Pl, mode, soft_iter, threshold, unit_cancel))
     return {k: np.concatenate([p[k] for p in parts], axis=0) for k in parts[0]}
 
 

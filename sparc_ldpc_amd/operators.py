@@ -228,6 +228,20 @@ class SparcOperator:
         check(self._lib.sa_decide(self._ctx, B, idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
         return idx
 
+    DECIDE_SLOTS = 4  # SA_DECIDE_SLOTS
+
+    def decide_async(self, B: int, slot: int) -> None:
+        """Queue the section argmax of the decode on the stream and the copy of
+        its (B, L) indices into pinned ring slot `slot`; returns at once."""
+        check(self._lib.sa_decide_async(self._ctx, int(B), int(slot)))
+
+    def decide_collect(self, B: int, slot: int) -> np.ndarray:
+        """Wait for slot `slot`'s decisions (decide_async) and return them, (B, L) int32."""
+        idx = np.empty((B, self.L), dtype=np.int32)
+        check(self._lib.sa_decide_collect(self._ctx, int(B), int(slot),
+                                          idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32))))
+        return idx
+
     # ---- device-resident path (bench) -------------------------------------
     def reserve(self, B, T):
         check(self._lib.sa_reserve(self._ctx, int(B), int(T)))
@@ -258,14 +272,19 @@ class SparcOperator:
     def profile(self, B, T, early_stop=True, beta0=False, rep=1):
         """Eager decode with per-launch HIP events: {kind: (mean_ms, launches)}, total_ms.
         rep > 1: each launch issued rep times back to back between its events
-        (mean = elapsed / rep; the staged results are then not a decode)."""
+        (mean = elapsed / rep; the staged results are then not a decode).
+        rep = 0: every loop kernel once, timed by the start / stop events of
+        its own dispatch (hipExtLaunchKernel; sa_profile_dispatch)."""
         flags = (0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP) | (_lib.SA_FLAG_BETA0 if beta0 else 0)
         nk = len(self.KERNEL_KINDS)
         if int(self._lib.sa_profile_kinds()) != nk:
             raise _lib.SparcAmpError(_lib.SA_ERR_UNSUPPORTED, f"libsparc_amp profiles {self._lib.sa_profile_kinds()} kernel kinds, "
                                 f"this module knows {nk}: rebuild the library")
         out = np.zeros(2 * nk + 1)
-        check(self._lib.sa_profile_rep(self._ctx, int(B), int(T), flags, int(rep), dptr(out)))
+        if rep == 0:
+            check(self._lib.sa_profile_dispatch(self._ctx, int(B), int(T), flags, dptr(out)))
+        else:
+            check(self._lib.sa_profile_rep(self._ctx, int(B), int(T), flags, int(rep), dptr(out)))
         kinds = {k: (float(out[2 * i]), int(out[2 * i + 1])) for i, k in enumerate(self.KERNEL_KINDS)}
         return kinds, float(out[2 * nk])
 

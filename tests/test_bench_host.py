@@ -22,11 +22,15 @@ class FakeOp:
     plan / profile data (a k_sec4 + k_row2 decode of T iterations)."""
     KERNEL_KINDS = ("k_sec", "k_row", "k_dense_az", "k_dense_den", "k_dense_ab", "k_i8_quant")
 
+    DECIDE_SLOTS = 4
+
     def __init__(self, L, M, n, backend, precision, device, plan):
         self.L, self.M, self.n = L, M, n
         self.w = 2 ** int(np.ceil(np.log2(max(M + 1, n + 1))))
         self.backend, self.precision = backend, precision
         self.runs = 0
+        self.log = []  # (call, perf_counter) of run / decide_async / decide_collect
+        self.slots = {}
 
     def Ab_batch(self, beta):
         return np.zeros((beta.shape[0], self.n))
@@ -39,7 +43,18 @@ class FakeOp:
 
     def run(self, B, T, early_stop=True, beta0=False):
         self.runs += 1
+        self.log.append(("run", time.perf_counter()))
         time.sleep(0.001)
+
+    def decide_async(self, B, slot):
+        assert slot not in self.slots, "slot reused before it was collected"
+        self.slots[slot] = B
+        self.log.append(("decide_async", time.perf_counter()))
+
+    def decide_collect(self, B, slot):
+        assert self.slots.pop(slot) == B
+        self.log.append(("decide_collect", time.perf_counter()))
+        return np.zeros((B, self.L), dtype=np.int32)
 
     def wait(self):
         pass
@@ -100,8 +115,49 @@ def test_n_rank_bench_line_carries_cpu_baseline_and_spread(world):
     assert r["kernel"] == "k_sec4" and r["bound"] == "hbm" and 0 < r["frac"] < 1
     assert r["consistency"]["T"] == 64 and r["consistency"]["per_iteration_ms"] > 0
     assert "sources" in r and line["fp64_leg"]["roofline"]["kernel"] == "k_sec4"
+    assert r["frac_dispatch"] > 0 and r["frac_events"] > 0 and "timing" in r
+    # every rank's timed steps were decided and counted
+    assert line["decisions"]["decided_steps"] == world * 4
+    assert line["decode_only"]["value"] > 0
     # the other ranks return the same line without printing it
     for r in range(1, world):
         assert json.loads(got[r])["value"] == line["value"]
     # value = every rank's codewords over the slowest rank's time
     assert abs(line["value"] - world * pr["value_min"]) <= 1e-3 * line["value"]
+
+
+def test_timed_step_includes_the_decision():
+    """a benched step is sa_run + the device argmax + the
+    copy of the L section indices to the host; every timed step's decisions
+    are collected inside the timed region, the decisions of step k while
+    decode k + 1 is queued."""
+    sys.path.insert(0, ROOT)
+    import bench
+    op = FakeOp(8, 4, 32, "hadamard", "fp32", 0, None)
+    sent = np.zeros((3, 8), dtype=np.int32)
+    sent[1, 2] = 1  # one section of one codeword differs from the stand-in's all-zero decisions
+    steps, warmup = 5, 2
+    ts = bench.timed_steps(op, 3, 64, steps, warmup, sent)
+    inside = [(k, t) for k, t in op.log if ts["t0"] <= t <= ts["t1"]]
+    assert [k for k, _ in inside].count("run") == steps
+    assert [k for k, _ in inside].count("decide_async") == steps
+    assert [k for k, _ in inside].count("decide_collect") == steps
+    assert ts["decided_steps"] == steps and ts["section_errors"] == steps  # one error per step, scored
+    # pipelined: decode k + 1 is queued before the decisions of decode k are collected
+    seq = [k for k, _ in inside]
+    assert seq[:4] == ["run", "decide_async", "run", "decide_async"] and seq[4] == "decide_collect"
+    assert not op.slots  # nothing left uncollected
+    # decode-only timing: no decisions
+    op.log.clear()
+    ts0 = bench.timed_steps(op, 3, 64, steps, 0, decide=False)
+    assert [k for k, _ in op.log].count("decide_async") == 0 and ts0["decided_steps"] == 0
+
+
+def test_load_trace_reads_the_exclusive_duration():
+    """load_trace returns the exclusive in-graph median too (a
+    committed trace line carries both)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    tr = bench.load_trace("c2", "k_sec4")
+    assert tr is not None and tr["duration_ns"] > 0 and tr["launches"] > 0
+    assert tr["exclusive_ns"] is not None and tr["exclusive_ns"] > 0

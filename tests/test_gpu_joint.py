@@ -120,3 +120,60 @@ def test_sim_ldpc_bpsk_runs():
     ber_hi = sp.sim_ldpc(lp, np.sqrt((1 / 10 ** (3.0 / 20)) / 2), MIN_ERRORS=20, MAX_BLOCKS=2000, batch=256, seed=1)
     ber_lo = sp.sim_ldpc(lp, np.sqrt((1 / 10 ** (5.0 / 20)) / 2), MIN_ERRORS=20, MAX_BLOCKS=512, batch=256, seed=1)
     assert ber_hi > ber_lo >= 0.0
+
+
+def _batch_cases():
+    keys = _cases()
+    out = sorted({(k.split("|")[0], k.split("|")[1]) for k in keys})
+    return out
+
+
+def _per_rep_bers(r, j, mode, tb):
+    if mode == "originalHard":
+        return [r["amp"][j, 0] / tb, r["ldpc"][j, 0] / tb, r["ldpc_amp"][j] / tb if "ldpc_amp" in r else -1.0]
+    return [e / tb for e in r["amp"][j]] + [e / tb for e in r["ldpc"][j]]
+
+
+@pytest.mark.parametrize("tag,mode", _batch_cases())
+def test_joint_reps_as_one_batch(G, tag, mode):
+    """every reference rep of a (config, scheme) decoded
+    in ONE batch padded to 256 codewords (mc_joint: the benched shape, two
+    concurrent halves of 128 on their own streams), against the reference's
+    per-rep BERs with the bars of test_joint_reps_match_reference; at full
+    size (c5) also as one 256-codeword decoder."""
+    from sparc_ldpc_amd import joint
+    keys = [k for k in _cases() if k.startswith(f"{tag}|{mode}|")]
+    seeds = [int(k.split("|")[2]) for k in keys]
+    pad = [900_000 + i for i in range(256 - len(seeds))]
+    spp, lp = _params(G, tag)
+    jd, Pl = joint._setup(spp, lp, precision="fp64")
+    tb = jd.total_bits
+    runs = [True] + ([False] if tag == "c5" else [])
+    for pipe in runs:
+        r = joint.mc_joint(jd, Pl, spp.sigma, seeds + pad, mode, soft_iter=2, batch=256, pipeline=pipe)
+        assert r["amp"].shape[0] == 256
+        for j, key in enumerate(keys):
+            got = np.array(_per_rep_bers(r, j, mode, tb))
+            ref = G[key + "|ber"]
+            assert got[0] == ref[0], (key, pipe)
+            its = [int(G[key + f"|it{k}"][0]) for k in range(4) if key + f"|it{k}" in G]
+            if all(i < 200 for i in its):
+                np.testing.assert_array_equal(got, ref, err_msg=f"{key} pipeline={pipe}")
+            else:
+                assert np.max(np.abs(got - ref)) <= 0.03, (key, pipe)
+
+
+def test_pipeline_equals_one_decoder():
+    """JointPipeline (two halves, two threads, own streams) == one decoder over
+    the batch, every per-rep count, for the three schemes and an odd batch."""
+    import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd.joint import joint_decoder, mc_joint
+    spp = sp.SPARCParams(64, 16, 0.95, 4.0, 1.0, 30)
+    lp = sp.LDPCParams("802.16", "5/6", 8)
+    jd = joint_decoder(64, 16, 256, lp, 30, precision="fp64")
+    Pl = 4.0 / 64 * np.ones(64)
+    for mode in ("originalHard", "soft", "hard"):
+        a = mc_joint(jd, Pl, spp.sigma, range(300, 371), mode, batch=71, pipeline=False)
+        b = mc_joint(jd, Pl, spp.sigma, range(300, 371), mode, batch=71, pipeline=True)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (mode, k)

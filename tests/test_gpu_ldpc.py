@@ -179,9 +179,9 @@ def test_max_iter_and_errors(bp):
                                              ("802.16", "1/2", 96, 1.3), ("802.16", "5/6", 300, 3.2)])
 def test_tail_launches_bit_identical(bp, std, rate, z, ebno):
     """The tail launches (words still running after tail_at iterations spread
-    over several workgroups, one launch per iteration, the variable update
-    folded into the check kernel) against whole decodes in one workgroup per
-    word: app and iteration counts identical for every word, every decoder,
+    over several workgroups, a variable and a check launch per iteration)
+    against whole decodes in one workgroup per word: app and iteration
+    counts identical for every word, every decoder,
     with words that stop before, at and after the hand-off and words that run
     to max_iter; the straight-line (5/6), general (1/2: variable degrees up to
     11 and 6) and HBM-message (z = 300) kernels."""
@@ -228,3 +228,40 @@ def test_large_batch_runs_without_the_tail(bp):
     assert np.array_equal(IT[::8193], it8) and np.array_equal(A[::8193], a8)
     assert np.array_equal(IT.reshape(8, 8193), np.repeat(it8[:, None], 8193, axis=1))
 
+
+
+@pytest.mark.parametrize("std,rate,z,ebno", [("802.16", "5/6", 192, 3.2), ("802.16", "1/2", 96, 1.3)])
+def test_device_sized_tail_bit_identical(bp, std, rate, z, ebno):
+    """lb_run (the tail sized on the device, every iteration queued, no host
+    wait; what the joint decoder uses) against lb_decode (the tail sized on
+    the host from one read-back): app and iteration counts identical, for
+    batches whose share of words entering the tail differs from the previous
+    call's estimate (all, some, none), and for max_iter cut inside the tail."""
+    c = bp.code(std, rate, z)
+    rs = np.random.RandomState(21)
+    X, CH = _awgn(c, rs, ebno, 40)
+    CH[:6] = 10 * (0.5 - X[:6])  # stop at iteration 0
+    easy = 10 * (0.5 - X)  # every word done before the tail
+    for algo in ["sumprod2", "sumprod"]:
+        for ch, mi in ((CH, 200), (easy, 200), (CH[6:], 200), (CH, 13)):
+            A0, I0 = c.decode_batch(ch, algo, max_iter=mi)
+            B = ch.shape[0]
+            d_ch, d_app, d_it = c.device_buffers(B)
+            lib = bp.load_bp_library()
+            assert lib.lb_stage(c._context(), B, np.ascontiguousarray(ch).ctypes.data_as(ct.POINTER(ct.c_double))) == 0
+            c.run_buffers(B, algo, max_iter=mi)
+            A1, I1 = c.fetch_buffers(B)
+            assert np.array_equal(I0, I1), (algo, mi)
+            assert np.array_equal(A0, A1, equal_nan=True), (algo, mi)
+
+
+def test_set_tail_default_restores_create_choice(bp, monkeypatch):
+    """lb_set_tail(-1) restores the tail chosen at lb_create, including an
+    LDPC_BP_TAIL override read there."""
+    monkeypatch.setenv("LDPC_BP_TAIL", "5")
+    c = bp.code("802.16", "5/6", 24)
+    assert c.info()["tail_at"] == 5
+    c.set_tail(0)
+    assert c.info()["tail_at"] == 0
+    c.set_tail(-1)
+    assert c.info()["tail_at"] == 5

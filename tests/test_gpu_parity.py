@@ -529,7 +529,16 @@ def test_profile_rep_and_plan(sp, B):
     kinds_rep, _ = op.profile(B, 2, early_stop=False, rep=8)
     assert kinds_rep["k_sec"][0] > 0 and kinds_rep["k_sec"][1] == 2
     with pytest.raises(AssertionError):  # SA_ERR_ARG: the reference's AssertionError cases
-        op.profile(B, T, rep=0)
+        op.profile(B, T, rep=-1)
+    # dispatch-bound events (sa_profile_dispatch): one pair per loop launch,
+    # and the decode it leaves behind is a decode (bit-identical to sa_run's)
+    kinds_d, total_d = op.profile(B, T, early_stop=False, rep=0)
+    assert kinds_d["k_sec"][1] == T and kinds_d["k_row"][1] == T + 1 and total_d > 0
+    assert 0 < kinds_d["k_sec"][0] <= total_d and 0 < kinds_d["k_row"][0] <= total_d
+    prof_beta, _ = op.fetch(B)
+    op.run(B, T, early_stop=False)
+    run_beta, _ = op.fetch(B)
+    assert np.array_equal(prof_beta, run_beta)
     bb, _ = op.amp_batch(ys, Pl, T, early_stop=False)
     for i in range(B):
         ref, _ = orc.amp_test(ys[i], 0, Pl, L, M, T, Ab, Az)
@@ -791,3 +800,32 @@ def test_batched_work_order_passes_bit_identical(sp, prec):
     ba, ia = a.amp_batch(ys, Pl, T, early_stop=False)
     bb, ib = b.amp_batch(ys, Pl, T, early_stop=False)
     assert np.array_equal(ba, bb) and np.array_equal(ia, ib)
+
+
+@pytest.mark.parametrize("B", [1, 8])
+def test_decide_async_matches_decide(sp, B):
+    """sa_decide_async / sa_decide_collect (the bench's pipelined decision):
+    the same indices as sa_decide, per slot, with decode k + 1 queued before
+    the decisions of decode k are collected; a slot holds one batch and a
+    collect of an empty slot is refused."""
+    L, M, T = 32, 64, 12
+    n = int(L * np.log2(M))
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n))
+    Pl = 4.0 / L * np.ones(L)
+    Ab, _, _ = orc.sparc_transforms(L, M, n)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.3, Ab, 300 + i)[1].reshape(-1) for i in range(B)])
+    op.reserve(B, T)
+    op.stage(ys, Pl)
+    op.run(B, T)
+    ref = op.decide(B)
+    op.run(B, T)
+    op.decide_async(B, 0)
+    op.run(B, T)
+    op.decide_async(B, 1)
+    a = op.decide_collect(B, 0)
+    b = op.decide_collect(B, 1)
+    assert np.array_equal(a, ref) and np.array_equal(b, ref)
+    with pytest.raises(AssertionError):
+        op.decide_collect(B, 0)  # already collected
+    with pytest.raises(AssertionError):
+        op.decide_async(B, op.DECIDE_SLOTS)

@@ -117,6 +117,7 @@ class JointDecoder:
         self.total_bits = self.L * self.logm
         self.R = (self.L * self.logm - (code.N - code.K)) / n  # sparc_ldpc.py:541
         self._masked = None  # full-size operator for the per-codeword masked decodes (threshold mode)
+        self._after_first_amp = None  # JointPipeline's stagger signal
 
     # -- message / channel draws (the reference's order) --------------------------
     def draw(self, rs, B, sigma):
@@ -167,6 +168,8 @@ class JointDecoder:
         op, T, l0 = self.op, self.T, self.l0
         op.run(B, T)
         op.wait()
+        if self._after_first_amp is not None:
+            self._after_first_amp()
         rx = op.decide(B)
         errs_amp = [self._errs(idx, rx)]
         errs_ldpc = []
@@ -314,9 +317,28 @@ class JointPipeline:
         self._map(lambda part, sl: part.stage(idx[sl], noise[sl], Pl))
 
     def decode_staged(self, idx, Pl, mode="soft", soft_iter=2, threshold=0.5, unit_cancel=False):
+        """The slices start staggered: slice i + 1 starts when slice i's first
+        AMP decode has finished, so that slice i's first BP (and every later
+        stage) falls beside slice i + 1's AMP instead of beside its own twin."""
+        import threading
         idx = np.ascontiguousarray(idx, dtype=np.int32)
         assert self._slices is not None and self._slices[-1].stop == idx.shape[0], "stage the batch first"
-        outs = self._map(lambda part, sl: part.decode_staged(idx[sl], Pl, mode, soft_iter, threshold, unit_cancel))
+        go = [threading.Event() for _ in self.parts]
+        go[0].set()
+
+        def one(part, sl):
+            i = self.parts.index(part)
+            go[i].wait()
+            nxt = go[i + 1] if i + 1 < len(go) else None
+            part._after_first_amp = nxt.set if nxt is not None else None
+            try:
+                return part.decode_staged(idx[sl], Pl, mode, soft_iter, threshold, unit_cancel)
+            finally:
+                part._after_first_amp = None
+                if nxt is not None:
+                    nxt.set()  # never leave the next slice waiting (an error, or a mode without that AMP)
+
+        outs = self._map(one)
         return {k: np.concatenate([o[k] for o in outs], axis=0) for k in outs[0]}
 
     def run(self, idx, noise, Pl, mode="soft", soft_iter=2, threshold=0.5, unit_cancel=False):

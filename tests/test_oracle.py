@@ -88,6 +88,23 @@ def test_c2_decode_matches_reference():
     assert np.array_equal(orc.section_argmax(b, L, M), g["argmax_final"])
 
 
+def test_c2_section_stats_match_reference():
+    """sections.npz (make_section_stats.py, the reference's own decode): the
+    oracle's per-section statistics of every C2 section at t = 1 and 8 are
+    the reference's bit for bit (the GPU tests hold the device to them)."""
+    g = golden("c2.npz")
+    S = golden("sections.npz")
+    L, M, n = int(g["L"]), int(g["M"]), int(g["n"])
+    Ab, Az, _ = orc.sparc_transforms(L, M, n)
+    Pl = float(g["P"]) / L * np.ones(L)
+    for t in (1, 8):
+        b = orc.amp(g["y"], 0, Pl, L, M, t, Ab, Az).reshape(L, M)
+        assert np.array_equal((b * b).sum(axis=1), S[f"c2_t{t}_e2"]), t
+        assert np.array_equal((b * np.arange(M)[None, :]).sum(axis=1), S[f"c2_t{t}_m1"]), t
+        assert np.array_equal(b.max(axis=1), S[f"c2_t{t}_mx"]), t
+    assert int(S["c2_t_stop"]) == int(g["t_stop"])
+
+
 def test_c5_draw_order_and_one_decode():
     """The harness draw order (np.random.seed -> randint bits -> randn noise,
     sparc_ldpc.py:423-446) and one full decode against amp_ldpc_sim."""

@@ -279,7 +279,8 @@ int sa_host_residual(sa_ctx* ctx, int B, int t, int flags, const double* ab);
 /* Introspection. */
 /* The kernels a decode of B codewords runs: out8 = {section kernel (0 k_sec,
  * 1 k_sec2, 2 k_secb, 3 dense fp32 GEMVs, 4 k_sec4, 5 k_sec43, 6 dense int8
- * MFMA GEMMs, 7 caller-matrix f32 / f64 MFMA GEMMs), Ab partials per codeword, row splits,
+ * MFMA GEMMs, 7 caller-matrix f32 / f64 MFMA GEMMs, 8 k_secg: z from global
+ * memory, 32-bit bucket entries, for n past the LDS image or >= 65535), Ab partials per codeword, row splits,
  * codewords per batched workgroup, z^2 partials, w, row kernel (1 k_row2,
  * 2 k_rowv 16-byte rows, 3 k_rowv 8-byte rows, 0 k_row, 4 k_row2 16-row
  * blocks, 5 k_rowc), number of CUs}. */

@@ -18,7 +18,7 @@ import json, sys
 try:
     d = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
     r = d["roofline"]
-    print(f"{sys.argv[1]:50s} {sys.argv[2]} {d['value']:10.1f} cw/s  {d['ms_per_step']:.4f} ms/step  {r['kernel']} {r['kernel_ms']}")
+    print(f"{sys.argv[1]:50s} {sys.argv[2]} {d['value']:10.1f} cw/s  {d['ms_per_step']:.4f} ms/step  {r['kernel']} {r.get('kernel_ms_dispatch')}")
 except Exception as e:
     print(sys.argv[1], sys.argv[2], "FAILED", e)
 PY

@@ -323,8 +323,20 @@ struct TailArgs {
   int* lastbad;          // [2][B]
   int Nv, Nc, Nmsg, B, n, S, it;
   int dyn;               // 1: n and the stop test from device memory
+  int prio;              // 1: the waves raise their issue priority (tail_prio)
   double corr;
 };
+
+// Issue priority of the tail's waves on their SIMDs.  Beside another stream's
+// full-chip kernel (the other slice of a pipelined joint batch: k_secb holds
+// every CU's LDS but leaves VGPRs for a few more waves per SIMD) the tail's
+// waves land on SIMDs shared with its waves, and at equal priority the
+// dependent Lxor chains get a fraction of the issue slots: an iteration ran
+// ~3x longer.  The highest wave priority lets them issue first (their chains
+// use a small share of the slots); results are unaffected.
+__device__ __forceinline__ void tail_prio(const TailArgs& a) {
+  if (a.prio) __builtin_amdgcn_s_setprio(3);
+}
 
 // words still running in this tail launch; 0 when every word is done
 __device__ __forceinline__ int tail_words(const TailArgs& a) {
@@ -337,6 +349,7 @@ __device__ __forceinline__ int tail_words(const TailArgs& a) {
 // and message loaded at once, summed in port order with exact selects
 template <int DV>
 __global__ void __launch_bounds__(256) k_bp_tail_var(TailArgs a) {
+  tail_prio(a);
   const int n = tail_words(a);
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   for (int wi = blockIdx.y; wi < n; wi += gridDim.y) {
@@ -381,6 +394,7 @@ template <int ALGO, int DCMAX, int DCFIX>
 __global__ void __launch_bounds__(DCFIX > 0 ? kTailFixThreads : kTailThreads) k_bp_tail_chk(TailArgs a) {
   constexpr int ROW = DCMAX + 1;
   __shared__ double rows[DCFIX > 0 ? 1 : kTailThreads * ROW];
+  tail_prio(a);
   const int n = tail_words(a);
   const int cpw = (a.Nc + a.S - 1) / a.S;
   for (int item = blockIdx.x; item < n * a.S; item += gridDim.x) {
@@ -551,6 +565,7 @@ struct lb_ctx {
   int est_n = 0, est_B = 0, est_Bq = 0;  // the last landed count and its batch; the batch in flight
   int capTailB = 0;
   int tail_default = 0;       // tail_at chosen at lb_create (kTailAt or LDPC_BP_TAIL)
+  int wave_prio = 1;          // tail waves at the highest issue priority (LDPC_BP_WAVE_PRIO=0: off)
   int* d_vedge = nullptr;
   uint8_t* d_vdeg = nullptr;
   int* d_cstart = nullptr;
@@ -754,6 +769,7 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.n = n;
   t.S = S;
   t.dyn = sized_on_host ? 0 : 1;
+  t.prio = c->wave_prio;
   t.corr = corr;
   double* slot[2] = {c->d_msg, c->d_msg + (size_t)B * c->Nmsg};
   const TailFn chk = pick_tail(algo, c->maxdc, split);
@@ -940,6 +956,10 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
     c->tail_at = (e && *e) ? std::max(0, atoi(e)) : kTailAt;
   }
   c->tail_default = c->tail_at;
+  {
+    const char* wp = getenv("LDPC_BP_WAVE_PRIO");
+    c->wave_prio = (wp && *wp && atoi(wp) == 0) ? 0 : 1;
+  }
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };
   if (hipSetDevice(device) != hipSuccess) return bail(fail(LB_ERR_HIP, "hipSetDevice failed"));

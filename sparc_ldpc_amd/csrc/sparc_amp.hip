@@ -79,6 +79,15 @@ __device__ __forceinline__ T ld_vmem(const T* p) {
   return p[z0];
 }
 
+// Load of a uniform value through the scalar cache (constant address space):
+// no VGPRs; only for values written before the kernel started (the scalar
+// cache is invalidated at dispatch) and read where no LDS access is in flight
+// (lgkmcnt is shared with LDS).
+template <typename T>
+__device__ __forceinline__ T ld_smem(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)(p);
+}
+
 // load at a uniform base + 32-bit byte offset (SGPR-base addressing, no
 // 64-bit address arithmetic per load)
 template <typename T>
@@ -774,6 +783,7 @@ struct SecArgs {
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
   const uint32_t* __restrict__ fwd3; // [ceil(L/3)][n] a section triple, 10-bit fields k | sign<<9 (M <= 512)
+  const uint32_t* __restrict__ inv32;  // [L][w] k_secg: inv with 32-bit rows (n >= 65535 or z past the LDS)
   const real* __restrict__ c;        // [L] sqrt(n * Pl), or [B][L] per codeword (cst = L)
   const real* __restrict__ z;        // [B][n]
   real* __restrict__ beta;           // [B][L*M] previous estimate (read)
@@ -1243,6 +1253,124 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
 #endif
 }
 
+
+// ---------------------------------------------------------------------------
+// Section kernel for operators whose z does not fit the section kernels' LDS
+// image (n past ~38000 in binary32), including every n >= 65535, whose row
+// indices need more than the 16-bit bucket entries: k_sec's structure (4
+// sections per workgroup, one wave each, RS workgroups splitting the rows,
+// sparc_ldpc.py:120-134 per section) with the bucket gather reading z from
+// global memory (one codeword's z, 4 or 8 B x n, stays in the XCD's L2)
+// through 32-bit entries inv32 [L][w] (row index, or n for an empty slot,
+// which contributes 0).  The sums run in h order, as in k_sec.  LDS holds
+// only the 4 sections' T = H_M beta (Ab partials) and their beta^2.
+// ---------------------------------------------------------------------------
+template <typename real, int E>
+__global__ void __launch_bounds__(256) k_secg(SecArgs<real> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int g = blockIdx.x / a.RS, rsi = blockIdx.x % a.RS;
+  const int b = blockIdx.y;
+  const int rows_per = (a.n + a.RS - 1) / a.RS;
+  const int rb0 = rsi * rows_per, rb1 = min(a.n, rb0 + rows_per);
+  const bool owner = rsi == 0;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int M = a.M, n = a.n;
+  const size_t LM = (size_t)a.L * M;
+  const int mlanes = M < 64 ? M : 64;
+  const int l = g * kSpw + wv;
+  const bool have = l < a.L;
+  const int lc = have ? l : a.L - 1;
+  real* ts = reinterpret_cast<real*>(smem);  // [kSpw][M]
+  real* bbw = ts + kSpw * M;                 // [kSpw]
+  real v[E];
+  real* bl = a.beta + (size_t)b * LM + (size_t)lc * M;
+  real* blo = a.beta_out + (size_t)b * LM + (size_t)lc * M;
+  if (a.mode == SEC_AB) {
+    load_section<real, E>(bl, v, lane, M);
+  } else {
+    real bprev[E];
+    real tau2 = 1;
+    const real cl = ld_vmem(a.c + (size_t)b * a.cst + lc);
+    if (a.mode == SEC_AMP) {
+      const real* zzb = a.zzp + (size_t)b * a.NZ;
+      const real tau = tau_from_parts(zzb, a.NZ, n);  // sparc_ldpc.py:203
+      const real last = a.t > 0 ? a.tau[(size_t)b * a.T1 + a.t - 1] : (real)0;
+      const bool stop = a.early_stop && (tau == last);  // :204-209
+      if (blockIdx.x == 0 && tid == 0) {
+        a.tau[(size_t)b * a.T1 + a.t] = tau;
+        if (stop && a.iters[b] < 0) a.iters[b] = a.t;
+      }
+      if (stop) return;  // uniform over the grid row: beta, z stay as they are
+      tau2 = tau * tau;
+      load_section<real, E>(bl, bprev, lane, M);
+    }
+    // bucket gather (:128-134): v[k] = sum_h sgn(h) z[inv[h M + k]], h order
+    const real* zb = a.z + (size_t)b * n;
+    const uint32_t* il = a.inv32 + (size_t)lc * a.w;
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = 0;
+    for (int h = 0; h < a.nhi; ++h) {
+      const bool neg = __popc(h) & 1;
+      const uint32_t* ih = il + (size_t)h * M;
+      real zv[E];
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        const int e = elem_index<E>(lane, i);
+        const uint32_t r = ih[e < M ? e : 0];
+        zv[i] = (e < M && r < (uint32_t)n) ? zb[r] : (real)0;
+      }
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[i] += neg ? -zv[i] : zv[i];
+    }
+    fwht_wave<real, E>(v, lane, E >= 2 ? 64 : mlanes);
+    if (a.mode == SEC_AZ) {
+      if (have && owner) {
+        real* ol = a.out + (size_t)b * LM + (size_t)l * M;
+#pragma unroll
+        for (int i = 0; i < E; ++i) v[i] = v[i] / a.sqrt_n;
+        store_section<real, E>(ol, v, lane, M);
+      }
+      return;  // uniform: no barrier follows in this mode
+    }
+    if (have) {
+      const real bb = denoise_section<real, E>(v, bprev, blo, lane, M, cl, tau2, a.sqrt_n, owner);
+      if (lane == 0) bbw[wv] = bb;
+    }
+  }
+  if (have) {
+    fwht_wave<real, E>(v, lane, E >= 2 ? 64 : mlanes);  // T_l = H_M beta_l
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = 0;
+    if (lane == 0) bbw[wv] = 0;
+  }
+  {
+    real* tl = ts + wv * M;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const int e = elem_index<E>(lane, i);
+      if (e < M) tl[e] = v[i];
+    }
+  }
+  __syncthreads();
+  if (a.mode == SEC_AMP && tid == 0 && owner)
+    a.bbp[(size_t)b * a.G + g] = ((bbw[0] + bbw[1]) + bbw[2]) + bbw[3];
+  // Ab partial of the group's 4 sections for this workgroup's rows (:120-126)
+  const ushort4* fw = a.fwd + (size_t)g * n;
+  real* abp = a.abp + ((size_t)b * a.G + g) * n;
+  for (int r = rb0 + tid; r < rb1; r += 256) {
+    const ushort4 f = fw[r];
+    const real v0 = ts[0 * M + (f.x & 0x7fffu)];
+    const real v1 = ts[1 * M + (f.y & 0x7fffu)];
+    const real v2 = ts[2 * M + (f.z & 0x7fffu)];
+    const real v3 = ts[3 * M + (f.w & 0x7fffu)];
+    real t = (f.x & 0x8000u) ? -v0 : v0;
+    t += (f.y & 0x8000u) ? -v1 : v1;
+    t += (f.z & 0x8000u) ? -v2 : v2;
+    t += (f.w & 0x8000u) ? -v3 : v3;
+    st_part(&abp[r], t);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Single-codeword section kernel, two wavefronts per section (M >= 128)
@@ -1838,6 +1966,15 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
     for (int c = 0; c < CB; ++c) v[c][i] = fma(zz[i][c], sg, v[c][i]);
 }
 
+#ifndef SA_F64_KH
+#define SA_F64_KH 1
+#endif
+#ifndef SA_F64_LATE_F
+#define SA_F64_LATE_F 0
+#endif
+#ifndef SA_F64_SLAST
+#define SA_F64_SLAST 0
+#endif
 template <typename real, int E, int CB, int W, bool ZIL = false>
 __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1847,7 +1984,10 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   constexpr bool F64 = sizeof(real) == 8;
   // bucket h-steps with table loads in flight together (binary64: one, which keeps
   // the kernel within 128 VGPRs without spills: C3 fp64 +3.5 %)
-  constexpr int KH = F64 ? 1 : ((E >= 16 || CB >= 4) ? 2 : 4);
+  constexpr int KH = F64 ? SA_F64_KH : ((E >= 16 || CB >= 4) ? 2 : 4);
+  // binary64: the first Ab-table rows loaded after the gather instead of with
+  // the first loads (their registers are then free for the table stream)
+  constexpr bool LATE_F = F64 && SA_F64_LATE_F;
   // rows per thread whose Ab-table loads are in flight together (one with 16
   // sections at CB = 4: their 4 table words per row already fill the registers)
   constexpr int KR = (CB >= 4 || F64) ? (W > 8 && (CB >= 4 || F64) ? 1 : 2) : 3;
@@ -1948,6 +2088,10 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   if constexpr (!F64) {
 #pragma unroll
     for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+  } else if constexpr (SA_F64_SLAST) {
+    // binary64: through the scalar cache, no VGPRs (tau_{t-1} was written by the previous launch)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_smem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
   }
   // z rows of the CB codewords (first pass of the staging loop)
   constexpr int KZ = 4;
@@ -1990,12 +2134,15 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   for (int c = 0; c < CB; ++c) cl[c] = ld_vmem(a.c + (size_t)bc[c] * a.cst + lc);
   const ushort4* fw = a.fwd + (size_t)g * W4 * n;
   ushort4 f[KR][W4];
+  auto load_f = [&]() {
 #pragma unroll
-  for (int u = 0; u < KR; ++u) {
-    const int r = u * NT + tid;
+    for (int u = 0; u < KR; ++u) {
+      const int r = u * NT + tid;
 #pragma unroll
-    for (int q = 0; q < W4; ++q) f[u][q] = fw[(size_t)q * n + (r < n ? r : 0)];
-  }
+      for (int q = 0; q < W4; ++q) f[u][q] = fw[(size_t)q * n + (r < n ? r : 0)];
+    }
+  };
+  if constexpr (!LATE_F) load_f();
   // tau per codeword (sparc_ldpc.py:203-209)
   bool live[CB];
   bool any = false;
@@ -2003,7 +2150,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     const real tau = zzc[c].tau(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
-    if constexpr (F64) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+    if constexpr (F64 && !SA_F64_SLAST) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
     const bool stop = a.early_stop && (tau == lastv[c]);
     if (valid[c] && g == 0 && tid == 0) {
       a.tau[(size_t)bc[c] * a.T1 + a.t] = tau;
@@ -2088,6 +2235,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       }
     }
   }
+  if constexpr (LATE_F) load_f();
   STAMP(3);
   // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
   // codewords with their section max / sums reduced together (wave_reduce_cb)
@@ -3104,6 +3252,11 @@ struct sa_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint16_t* d_inv = nullptr;
+  // operators whose z does not fit the section kernels' LDS (n >= 65535, or
+  // the z image past 160 KB): k_secg with 32-bit bucket entries, no batched /
+  // multi-wave kernels
+  bool big = false;
+  uint32_t* d_inv32 = nullptr;
   uint16_t* d_invb = nullptr;  // k_secb's bank-aware bucket table (build_invb), built on first batched use
   bool invb_done = false;
   uint16_t* d_fwd = nullptr;
@@ -3387,7 +3540,7 @@ int download(sa_ctx* c, double* dst, const void* src, size_t count) {
 template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
-  a.inv = c->d_inv; a.invb = c->d_invb; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
+  a.inv = c->d_inv; a.inv32 = c->d_inv32; a.invb = c->d_invb; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
@@ -3432,7 +3585,10 @@ void launch_sec_e(sa_ctx* c, int B, SecArgs<real> a) {
   a.RS = row_splits(c, B);
   dim3 grid(c->G * a.RS, B);
   if (c->prof) c->prof->begin(c->stream, K_SEC);
-  plaunch(c, k_sec<real, E>, grid, 256, c->sec_lds, a);
+  if (c->big)
+    plaunch(c, k_secg<real, E>, grid, 256, c->sec_lds, a);
+  else
+    plaunch(c, k_sec<real, E>, grid, 256, c->sec_lds, a);
   if (c->prof) c->prof->end(c->stream);
 }
 
@@ -4136,9 +4292,43 @@ int set_power_batch(sa_ctx* c, int B, const double* Pl) {
   return SA_OK;
 }
 
+// Tables of a k_secg operator: the bucket table with 32-bit row entries and
+// the 4-section Ab table (k | sign << 15 per row, any n).
+int build_tables_big(sa_ctx* c) {
+  const int L = c->L, n = c->n, w = c->w, M = c->M;
+  const int lgM = ilog2(M);
+  std::vector<uint32_t> inv((size_t)L * w, (uint32_t)n);
+  const int G = (L + kSG - 1) / kSG * (kSG / kSpw);
+  std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);
+  for (int l = 0; l < L; ++l) {
+    const uint32_t* o = c->ordering.data() + (size_t)l * n;
+    uint32_t* il = inv.data() + (size_t)l * w;
+    for (int r = 0; r < n; ++r) {
+      const uint32_t v = o[r];
+      if (v == 0 || v >= (uint32_t)w)
+        return fail(SA_ERR_ORDERING, "ordering[" + std::to_string(l) + "," + std::to_string(r) +
+                                         "] = " + std::to_string(v) + " outside [1, w=" + std::to_string(w) + ")");
+      if (il[v] != (uint32_t)n)
+        return fail(SA_ERR_ORDERING, "ordering row " + std::to_string(l) + " repeats value " + std::to_string(v));
+      il[v] = (uint32_t)r;
+      const uint32_t hi = v >> lgM;
+      fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)] =
+          (uint16_t)((v & (uint32_t)(M - 1)) | ((__builtin_popcount(hi) & 1u) << 15));
+    }
+  }
+  int rc;
+  if ((rc = dev_alloc(c, (void**)&c->d_inv32, inv.size() * 4))) return rc;
+  if ((rc = dev_alloc(c, (void**)&c->d_fwd, fwd.size() * 2))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_inv32, inv.data(), inv.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_fwd, fwd.data(), fwd.size() * 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
 int build_tables(sa_ctx* c) {
   const int L = c->L, n = c->n, w = c->w, M = c->M;
   const int lgM = ilog2(M);
+  if (c->big) return build_tables_big(c);
   std::vector<uint16_t> inv((size_t)L * w, (uint16_t)n);
   const int G = (L + kSG - 1) / kSG * (kSG / kSpw);  // padded to whole batched groups
   std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);  // [G][n][4]; missing sections -> (k 0, +)
@@ -4358,6 +4548,8 @@ hipError_t lds_attr_all() {
 #define SA_A(F) if (e == hipSuccess) e = hipFuncSetAttribute((const void*)F, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
   SA_A((k_sec<real, 1>)) SA_A((k_sec<real, 2>)) SA_A((k_sec<real, 4>)) SA_A((k_sec<real, 8>))
   SA_A((k_sec<real, 16>)) SA_A((k_sec<real, 32>)) SA_A((k_sec<real, 64>))
+  SA_A((k_secg<real, 1>)) SA_A((k_secg<real, 2>)) SA_A((k_secg<real, 4>)) SA_A((k_secg<real, 8>))
+  SA_A((k_secg<real, 16>)) SA_A((k_secg<real, 32>)) SA_A((k_secg<real, 64>))
   SA_A((k_sec2<real, 1>)) SA_A((k_sec2<real, 2>)) SA_A((k_sec2<real, 4>)) SA_A((k_sec2<real, 8>))
   SA_A((k_sec2<real, 16>)) SA_A((k_sec2<real, 32>))
   SA_A((k_sec4<real, 1>)) SA_A((k_sec4<real, 2>)) SA_A((k_sec4<real, 4>)) SA_A((k_sec4<real, 8>))
@@ -4450,7 +4642,10 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   if (!pow2 && backend == SA_BACKEND_HADAMARD)
     return fail(SA_ERR_UNSUPPORTED, "the matrix-free Hadamard operator needs M a power of two "
                                     "(the dense and host-operator backends take any M)");
-  if (n >= 65535) return fail(SA_ERR_UNSUPPORTED, "n must be < 65535");
+  // the Hadamard operator takes n past 16-bit row indices (k_secg); the
+  // materialised designs and the host-operator loop keep the 16-bit limit
+  if (n >= (backend == SA_BACKEND_HADAMARD ? (1 << 24) : 65535))
+    return fail(SA_ERR_UNSUPPORTED, backend == SA_BACKEND_HADAMARD ? "n must be < 2^24" : "n must be < 65535");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SA_ERR_NO_DEVICE, "no HIP device visible");
   if (device < 0 || device >= ndev) return fail(SA_ERR_ARG, "device index out of range");
@@ -4475,13 +4670,19 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   const size_t s = rsz(c);
   const size_t zbytes = ((size_t)(n + 1) * s + 15) / 16 * 16;
   c->sec_lds = zbytes + (size_t)kSpw * M * s + (size_t)kSpw * s;
+  if (backend == SA_BACKEND_HADAMARD && (n >= 65535 || c->sec_lds > 160 * 1024)) {
+    // z from global memory, 32-bit bucket entries (k_secg); the multi-wave and
+    // batched kernels' LDS images need z too: they stay off (G2, CB below)
+    c->big = true;
+    c->sec_lds = (size_t)kSpw * M * s + (size_t)kSpw * s;
+  }
   if (c->sec_lds > 160 * 1024) {
     delete c;
     return fail(SA_ERR_UNSUPPORTED, "section kernel does not fit in LDS (n and M too large for this precision)");
   }
   c->G = (L + kSpw - 1) / kSpw;
   c->Gb = (L + kWB - 1) / kWB;  // (re-set after the batched width is chosen)
-  if (M >= 128 && M <= 4096) {  // k_sec2: z + 2 sections' T + top-bit exchange + reductions
+  if (M >= 128 && M <= 4096 && !c->big) {  // k_sec2: z + 2 sections' T + top-bit exchange + reductions
     const size_t need = zbytes + 2 * (size_t)M * s + 4 * (size_t)(M / 2) * s + 16 * s;
     if (need <= 160 * 1024) {
       c->G2 = (L + 1) / 2;
@@ -4528,7 +4729,8 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       }
       return {0, 0};
     };
-    const auto c8 = cb_for(kWB), c16 = cb_for(kWB16);
+    const auto c8 = c->big ? std::pair<int, size_t>{0, 0} : cb_for(kWB);
+    const auto c16 = c->big ? std::pair<int, size_t>{0, 0} : cb_for(kWB16);
     const bool w16 = (plan & SA_PLAN_WB16) ? true
                      : (plan & SA_PLAN_WB8) ? false
                                             : c16.first >= c8.first;
@@ -4942,6 +5144,7 @@ void sa_destroy(sa_ctx* c) {
   drop_graphs(c);
   free_workspace(c);
   dev_free(c->d_inv);
+  dev_free(c->d_inv32);
   dev_free(c->d_invb);
   dev_free(c->d_fwd);
   dev_free(c->d_fwd2);
@@ -5489,7 +5692,7 @@ int sa_plan(sa_ctx* c, int B, int64_t* o) {
   const bool sec2 = use_sec2(c, B);
   const bool i8 = use_i8(c, B);
   const bool fg = use_fgemm(c, B);
-  o[0] = i8 ? 6 : (fg ? 7 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? 5 : (c->sec4 ? 4 : 1)) : 0))));
+  o[0] = i8 ? 6 : (fg ? 7 : (dense ? 3 : (batched ? 2 : (sec2 ? (c->sec3 ? 5 : (c->sec4 ? 4 : 1)) : (c->big ? 8 : 0)))));
   o[1] = i8 ? i8_splits(c, B)
             : (fg ? fgemm_splits(c, B) : (dense ? c->KS : (batched ? c->Gb : (sec2 ? sec2_parts(c) : c->G))));
   o[2] = (!dense && !batched && !sec2) ? row_splits(c, B) : 1;

@@ -300,7 +300,8 @@ class SparcOperator:
         check(self._lib.sa_fetch(self._ctx, B, None, it.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int))))
         return it
 
-    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43", "dense_mfma", "matrix_mfma")
+    SECTION_KERNELS = ("k_sec", "k_sec2", "k_secb", "dense", "k_sec4", "k_sec43", "dense_mfma", "matrix_mfma",
+                       "k_secg")
 
     def fetch_z(self, B):
         """Residual z after the last decode's final iteration, (B, n)."""

@@ -436,8 +436,9 @@ def test_full_size_properties_c4(sp):
 def test_maximum_sizes_vs_oracle(sp, prec, L, M, n):
     """The largest n the section kernels stage in LDS (w up to 65536, the
     uint16 table limit): operator, single-codeword and batched decodes
-    against the oracle; one step past the LDS limit is refused with an error,
-    never launched."""
+    against the oracle; one step past the LDS limit runs on k_secg (z from
+    global memory, test_big_n_vs_oracle); the dense backend keeps the 16-bit
+    row limit and refuses n = 65535 with an error, never launched."""
     Ab, Az, ordering = sp.sparc_transforms(L, M, n, precision=prec)
     oAb, oAz, oord = orc.sparc_transforms(L, M, n)
     assert np.array_equal(ordering, oord)
@@ -457,11 +458,47 @@ def test_maximum_sizes_vs_oracle(sp, prec, L, M, n):
         assert rel(bb[0], ref) <= TOL[prec]
         ref4, _ = orc.amp_test(ys[4], 0, Pl, L, M, 4, oAb, oAz)
         assert rel(bb[4], ref4) <= TOL[prec]
+    assert op.plan(1)["section_kernel"] != "k_secg"
     too_big = {"fp32": 40000, "fp64": 19000}[prec] if M == 512 else 25000
-    with pytest.raises(sp.SparcAmpError):
-        sp.SparcOperator(L, M, too_big, sp.make_ordering(L, M, too_big), precision=prec)
-    with pytest.raises(sp.SparcAmpError):
-        sp.SparcOperator(2, 8, 65535, sp.make_ordering(2, 8, 65535), precision=prec)
+    big = sp.SparcOperator(L, M, too_big, sp.make_ordering(L, M, too_big), precision=prec)
+    assert big.plan(1)["section_kernel"] == "k_secg" and big.plan(8)["section_kernel"] == "k_secg"
+    if prec == "fp32":
+        with pytest.raises(sp.SparcAmpError):
+            sp.SparcOperator(2, 8, 65535, sp.make_ordering(2, 8, 65535), backend="dense", precision=prec)
+
+
+@pytest.mark.parametrize("prec,L,M,n", [("fp32", 6, 512, 70000),   # n past 16-bit rows, w = 131072
+                                         ("fp64", 4, 256, 40000),   # z past the binary64 LDS image
+                                         ("fp32", 5, 64, 100000)])  # E = 1, w = 131072
+def test_big_n_vs_oracle(sp, prec, L, M, n):
+    """the Hadamard operator past the 16-bit row tables
+    and the LDS image of z (k_secg: z from global memory, 32-bit bucket
+    entries): operator products, a T = 3 decode single and batched, and the
+    early stop against the oracle (sparc_ldpc.py:54 takes any n)."""
+    Ab, Az, ordering = sp.sparc_transforms(L, M, n, precision=prec)
+    oAb, oAz, oord = orc.sparc_transforms(L, M, n)
+    assert np.array_equal(ordering, oord)
+    op = sp.SparcOperator(L, M, n, ordering, precision=prec)
+    assert op.plan(1)["section_kernel"] == "k_secg"
+    rs = np.random.RandomState(n + L)
+    b = rs.randn(L * M, 1); z = rs.randn(n, 1)
+    assert rel(Ab(b), oAb(b)) <= TOL[prec]
+    assert rel(Az(z), oAz(z)) <= TOL[prec]
+    Pl = 3.0 / L * np.ones(L)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 40.0, oAb, 90 + i)[1].reshape(-1) for i in range(3)])
+    for T in (1, 3):
+        ref = orc.amp(ys[0], 0, Pl, L, M, T, oAb, oAz)
+        b1 = sp.amp(ys[0], 0, Pl, L, M, T, Ab, Az)
+        assert rel(b1, ref) <= TOL[prec] and argmax_agree(b1, ref, L, M), T
+    bb, _ = op.amp_batch(ys, Pl, 3, early_stop=False)
+    for i in range(3):
+        assert rel(bb[i], orc.amp(ys[i], 0, Pl, L, M, 3, oAb, oAz)) <= TOL[prec], i
+    # converged decode: the transmitted sections at high SNR
+    idx = rs.randint(0, M, L)
+    b0 = np.zeros((L * M, 1)); b0[np.arange(L) * M + idx, 0] = np.sqrt(n * Pl)
+    y = oAb(b0) + 0.1 * rs.randn(n, 1)
+    bf, t = sp.amp_test(y, 0.1, Pl, L, M, 20, Ab, Az, precision="operator")
+    assert np.array_equal(orc.section_argmax(bf, L, M), idx)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp64"])

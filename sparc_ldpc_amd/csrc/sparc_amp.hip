@@ -1975,6 +1975,9 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 #ifndef SA_F64_SLAST
 #define SA_F64_SLAST 0
 #endif
+#ifndef SA_GSIGN
+#define SA_GSIGN 0
+#endif
 template <typename real, int E, int CB, int W, bool ZIL = false>
 __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2195,7 +2198,9 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     for (int i = 0; i < E; ++i) v[c][i] = 0;
   {
     constexpr int Q = E < 4 ? E : 4;
-    for (int h0 = 0; h0 < a.nhi; h0 += KH) {
+    // one block of KH h-steps; sgf >= 0: every step of the block has that
+    // sign (the bank-aware order's halves), else sgn(h) per step
+    auto block = [&](int h0, int sgf) {
       ushort4 tn[KH][NQ];
       const bool more = h0 + KH < a.nhi;
       if (more) {
@@ -2210,7 +2215,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
         if (h0 + hh < a.nhi) {
           // sgn(h): the high index bits of w-M+c are all ones; in the bank-aware
           // order the slots of sign -1 are the second half of the steps
-          const bool neg = banked ? (h0 + hh >= (a.nhi >> 1)) : (__popc(h0 + hh) & 1);
+          const bool neg = sgf >= 0 ? sgf == 1 : (banked ? (h0 + hh >= (a.nhi >> 1)) : (__popc(h0 + hh) & 1));
           const real sg = neg ? -sgl : sgl;
           if constexpr (E >= 4) {
             gather_step4<real, E, CB>(reinterpret_cast<const unsigned char*>(zs), tb[hh], sg, v);
@@ -2233,9 +2238,17 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
 #pragma unroll
           for (int j = 0; j < NQ; ++j) tb[hh][j] = tn[hh][j];
       }
+    };
+    const int half = a.nhi >> 1;
+    if (SA_GSIGN && banked && half > 0 && half % KH == 0) {
+      // the bank-aware order: the +1 steps, then the -1 steps; the sign is a
+      // constant of each loop (the same fmas with the same signs)
+      for (int h0 = 0; h0 < half; h0 += KH) block(h0, 0);
+      for (int h0 = half; h0 < a.nhi; h0 += KH) block(h0, 1);
+    } else {
+      for (int h0 = 0; h0 < a.nhi; h0 += KH) block(h0, -1);
     }
   }
-  if constexpr (LATE_F) load_f();
   STAMP(3);
   // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
   // codewords with their section max / sums reduced together (wave_reduce_cb)

@@ -1868,9 +1868,11 @@ __global__ void __launch_bounds__(768) k_sec43(SecArgs<real> a) { secq_body<real
 // the XCD) so the group's tables stay in that XCD's L2.
 constexpr int kSG = 16;  // fwd table padding (sections)
 // table bytes of the section groups one XCD works on at a time (SecArgs::gpx).
-// C4 binary32 k_secb HBM bytes per launch (PMC, round 4): one pass (6 groups,
-// 4.7 MB) 1.715 GB; 2.5 MB -> 2 x 3 groups 1.495 GB; 1.7 MB -> 3 x 2 groups
-// 1.514 GB; 0.9 MB -> 6 x 1 group 1.711 GB (every pass re-reads z)
+// C4 binary32 k_secb HBM bytes per launch (PMC, round 4; the 1.7 / 0.9 MB
+// points on an intermediate build with an L2-budget switch since removed):
+// one pass (6 groups, 4.7 MB) 1.715 GB; 2.5 MB -> 2 x 3 groups 1.495 GB;
+// 1.7 MB -> 3 x 2 groups 1.514 GB; 0.9 MB -> 6 x 1 group 1.711 GB (every
+// pass re-reads z)
 constexpr size_t kSecbL2 = (size_t)5 << 19;  // 2.5 MB of the 4 MB L2
 // sections (waves) per batched workgroup: 8 (two workgroups per CU), or 16
 // (one per CU) where the wider workgroup's LDS holds a larger codeword chunk

@@ -1968,17 +1968,28 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
     for (int c = 0; c < CB; ++c) v[c][i] = fma(zz[i][c], sg, v[c][i]);
 }
 
+// Build-time switches of k_secb (A/B builds; the defaults are the measured
+// best, every combination bit-identical, scripts/run_r05h.sh):
+//   SA_F64_KH      binary64 bucket h-steps in flight (2 spills at 128 VGPRs)
+//   SA_F64_LATE_F  binary64: the first Ab-table rows loaded after the gather
+//   SA_F64_SLAST   binary64: tau_{t-1} through the scalar cache (no VGPRs, no
+//                  extra round trip after tau)
+//   SA_GSIGN       the gather's sign a constant of each half of the bank-aware
+//                  step order (two loops) instead of selected per step
+// Round 5, interleaved A/B x2: binary32 C3 14.55 k -> 14.96 k, C4 6.93 k ->
+// 7.12 k cw/s (SA_GSIGN); binary64 C3 7.03 k -> 7.33 k, C4 3.22 k -> 3.36 k
+// (all three; SA_GSIGN alone 7.21 k / 3.32 k).
 #ifndef SA_F64_KH
 #define SA_F64_KH 1
 #endif
 #ifndef SA_F64_LATE_F
-#define SA_F64_LATE_F 0
+#define SA_F64_LATE_F 1
 #endif
 #ifndef SA_F64_SLAST
-#define SA_F64_SLAST 0
+#define SA_F64_SLAST 1
 #endif
 #ifndef SA_GSIGN
-#define SA_GSIGN 0
+#define SA_GSIGN 1
 #endif
 template <typename real, int E, int CB, int W, bool ZIL = false>
 __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
@@ -2251,6 +2262,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       for (int h0 = 0; h0 < a.nhi; h0 += KH) block(h0, -1);
     }
   }
+  if constexpr (LATE_F) load_f();
   STAMP(3);
   // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
   // codewords with their section max / sums reduced together (wave_reduce_cb)

@@ -1970,17 +1970,19 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 
 // Build-time switches of k_secb (A/B builds; the defaults are the measured
 // best, every combination bit-identical, scripts/run_r05h.sh):
-//   SA_F64_KH      binary64 bucket h-steps in flight (2 spills at 128 VGPRs)
+//   SA_F64_KH      binary64 bucket h-steps in flight (2 once LATE_B frees the registers)
 //   SA_F64_LATE_F  binary64: the first Ab-table rows loaded after the gather
+//   SA_F64_LATE_B  binary64: codeword 0's previous estimate loaded after the gather
 //   SA_F64_SLAST   binary64: tau_{t-1} through the scalar cache (no VGPRs, no
 //                  extra round trip after tau)
 //   SA_GSIGN       the gather's sign a constant of each half of the bank-aware
 //                  step order (two loops) instead of selected per step
 // Round 5, interleaved A/B x2: binary32 C3 14.55 k -> 14.96 k, C4 6.93 k ->
 // 7.12 k cw/s (SA_GSIGN); binary64 C3 7.03 k -> 7.33 k, C4 3.22 k -> 3.36 k
-// (all three; SA_GSIGN alone 7.21 k / 3.32 k).
+// (all three; SA_GSIGN alone 7.21 k / 3.32 k); then LATE_B with KH = 2: C3
+// fp64 7.39 k -> 7.46 k, C4 fp64 3.38 k -> 3.46 k (LATE_B alone: neutral).
 #ifndef SA_F64_KH
-#define SA_F64_KH 1
+#define SA_F64_KH 2
 #endif
 #ifndef SA_F64_LATE_F
 #define SA_F64_LATE_F 1
@@ -1991,6 +1993,9 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 #ifndef SA_GSIGN
 #define SA_GSIGN 1
 #endif
+#ifndef SA_F64_LATE_B
+#define SA_F64_LATE_B 1
+#endif
 template <typename real, int E, int CB, int W, bool ZIL = false>
 __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1998,12 +2003,13 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   constexpr int NQ = (E + 3) / 4;
   // binary64: fewer loads in flight so a wave fits 128 VGPRs (two workgroups per CU)
   constexpr bool F64 = sizeof(real) == 8;
-  // bucket h-steps with table loads in flight together (binary64: one, which keeps
-  // the kernel within 128 VGPRs without spills: C3 fp64 +3.5 %)
+  // bucket h-steps with table loads in flight together (binary64: SA_F64_KH)
   constexpr int KH = F64 ? SA_F64_KH : ((E >= 16 || CB >= 4) ? 2 : 4);
   // binary64: the first Ab-table rows loaded after the gather instead of with
   // the first loads (their registers are then free for the table stream)
   constexpr bool LATE_F = F64 && SA_F64_LATE_F;
+  // binary64: the previous estimate of codeword 0 loaded after the gather too
+  constexpr bool LATE_B = F64 && SA_F64_LATE_B;
   // rows per thread whose Ab-table loads are in flight together (one with 16
   // sections at CB = 4: their 4 table words per row already fill the registers)
   constexpr int KR = (CB >= 4 || F64) ? (W > 8 && (CB >= 4 || F64) ? 1 : 2) : 3;
@@ -2142,7 +2148,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
 #pragma unroll
     for (int c = 0; c < CB; ++c)
       load_section_nt<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lpos, M);
-  } else {
+  } else if constexpr (!LATE_B) {
     load_section_nt<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lpos, M);
   }
   real cl[CB];
@@ -2263,6 +2269,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     }
   }
   if constexpr (LATE_F) load_f();
+  if constexpr (LATE_B) load_section_nt<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lpos, M);
   STAMP(3);
   // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
   // codewords with their section max / sums reduced together (wave_reduce_cb)

@@ -2259,7 +2259,10 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       }
     };
     const int half = a.nhi >> 1;
-    if (SA_GSIGN && banked && half > 0 && half % KH == 0) {
+    // (the 16-byte-row configurations up to M = 512: elsewhere the duplicated
+    // loop body spilled)
+    constexpr bool GS = SA_GSIGN && CB * sizeof(real) == 16 && E <= 8;
+    if (GS && banked && half > 0 && half % KH == 0) {
       // the bank-aware order: the +1 steps, then the -1 steps; the sign is a
       // constant of each loop (the same fmas with the same signs)
       for (int h0 = 0; h0 < half; h0 += KH) block(h0, 0);

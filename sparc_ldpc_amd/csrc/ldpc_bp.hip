@@ -333,7 +333,10 @@ struct TailArgs {
 // waves land on SIMDs shared with its waves, and at equal priority the
 // dependent Lxor chains get a fraction of the issue slots: an iteration ran
 // ~3x longer.  The highest wave priority lets them issue first (their chains
-// use a small share of the slots); results are unaffected.
+// use a small share of the slots); results are unaffected.  Measured neutral
+// (2113-2119 vs 2114-2115 codewords/s): the tail's launches wait for whole
+// CUs, not for issue slots (k_secb<double> holds every CU's registers), so it
+// stays off by default (LDPC_BP_WAVE_PRIO=1 turns it on).
 __device__ __forceinline__ void tail_prio(const TailArgs& a) {
   if (a.prio) __builtin_amdgcn_s_setprio(3);
 }
@@ -565,7 +568,7 @@ struct lb_ctx {
   int est_n = 0, est_B = 0, est_Bq = 0;  // the last landed count and its batch; the batch in flight
   int capTailB = 0;
   int tail_default = 0;       // tail_at chosen at lb_create (kTailAt or LDPC_BP_TAIL)
-  int wave_prio = 1;          // tail waves at the highest issue priority (LDPC_BP_WAVE_PRIO=0: off)
+  int wave_prio = 0;          // tail waves at the highest issue priority (LDPC_BP_WAVE_PRIO=1; measured neutral)
   int* d_vedge = nullptr;
   uint8_t* d_vdeg = nullptr;
   int* d_cstart = nullptr;
@@ -958,7 +961,7 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
   c->tail_default = c->tail_at;
   {
     const char* wp = getenv("LDPC_BP_WAVE_PRIO");
-    c->wave_prio = (wp && *wp && atoi(wp) == 0) ? 0 : 1;
+    c->wave_prio = (wp && *wp && atoi(wp) == 1) ? 1 : 0;
   }
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };

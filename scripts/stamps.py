@@ -16,7 +16,8 @@ if len(sys.argv) > 2:  # batch override (e.g. c4 1: the single-codeword k_sec43)
 L, M, P, T, B = w["L"], w["M"], w["P"], w["T"], w["B"]
 n = n_of(w)
 Pl = P / L * np.ones(L)
-op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=os.environ.get("STAMPS_PREC", "fp32"))
+op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=os.environ.get("STAMPS_PREC", "fp32"),
+                      plan=[p for p in os.environ.get("STAMPS_PLAN", "").split(",") if p])
 y = synth_y(op, Pl, w["sigma"], list(range(B)))
 op.reserve(B, T); op.stage(y, Pl)
 lib = sp.load_library()

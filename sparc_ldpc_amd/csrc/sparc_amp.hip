@@ -781,6 +781,10 @@ struct SecArgs {
   // k_secb: the bucket table in bank-aware step order (build_invb), or null
   const uint16_t* __restrict__ invb;
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
+  // k_secb's Ab table (build_fwdb): [Gb * W / 4][npad][4] with npad = n rounded
+  // up to 64; entry (s * M + k) | sign << 15 for the workgroup's local section
+  // s, each row's W entries in a bank-aware step order
+  const ushort4* __restrict__ fwdb;
   const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
   const uint32_t* __restrict__ fwd3; // [ceil(L/3)][n] a section triple, 10-bit fields k | sign<<9 (M <= 512)
   const uint32_t* __restrict__ inv32;  // [L][w] k_secg: inv with 32-bit rows (n >= 65535 or z past the LDS)
@@ -1956,6 +1960,10 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
   using V = real __attribute__((ext_vector_type(CB)));
   using lds_v = __attribute__((address_space(3))) const V;
   real zz[E][CB];
+#ifdef SA_DIAG_GATHER_NOCONF
+#pragma unroll
+  for (int i = 0; i < E; ++i) ad[i] = (((threadIdx.x & 15) + 16 * i) << SH) + (ad[i] & 0);
+#endif
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const V x = *reinterpret_cast<lds_v*>((size_t)ad[i]);
@@ -2154,14 +2162,17 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   real cl[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) cl[c] = ld_vmem(a.c + (size_t)bc[c] * a.cst + lc);
-  const ushort4* fw = a.fwd + (size_t)g * W4 * n;
+  // the Ab table rows: [W4][npad] of this group (rows past npad: whole waves,
+  // every lane reading row 0, a broadcast)
+  const int npad = (n + 63) & ~63;
+  const ushort4* fw = a.fwdb + (size_t)g * W4 * npad;
   ushort4 f[KR][W4];
   auto load_f = [&]() {
 #pragma unroll
     for (int u = 0; u < KR; ++u) {
       const int r = u * NT + tid;
 #pragma unroll
-      for (int q = 0; q < W4; ++q) f[u][q] = fw[(size_t)q * n + (r < n ? r : 0)];
+      for (int q = 0; q < W4; ++q) f[u][q] = fw[(size_t)q * npad + (r < npad ? r : 0)];
     }
   };
   if constexpr (!LATE_F) load_f();
@@ -2360,8 +2371,9 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   }
   STAMP(5);
   // ---- Ab partial of the workgroup's W sections for every row ---------------
+  // (each row's W table entries in its own bank-aware order, build_fwdb: the
+  // entry holds the staged T element s * M + k itself)
   constexpr int SHB = ilog2c<CB * (int)sizeof(real)>();      // T element k -> byte k << SHB
-  const unsigned secb = (unsigned)M * CB * (unsigned)sizeof(real);  // bytes per staged section
   for (int r0 = 0; r0 < n; r0 += KR * NT) {
     ushort4 fn[KR][W4];
     const bool more = r0 + KR * NT < n;
@@ -2370,7 +2382,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       for (int u = 0; u < KR; ++u) {
         const int r = r0 + KR * NT + u * NT + tid;
 #pragma unroll
-        for (int q = 0; q < W4; ++q) fn[u][q] = fw[(size_t)q * n + (r < n ? r : 0)];
+        for (int q = 0; q < W4; ++q) fn[u][q] = fw[(size_t)q * npad + (r < npad ? r : 0)];
       }
     }
 #pragma unroll
@@ -2398,14 +2410,18 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
             using V = real __attribute__((ext_vector_type(CB)));
             using lds_v = __attribute__((address_space(3))) const V;
             // ts is LDS address 0 (the dynamic region, no static LDS)
-            const V x = *reinterpret_cast<lds_v*>((size_t)((k << SHB) + (unsigned)(q * 4 + s4) * secb));
+#ifdef SA_DIAG_ROWS_NOCONF
+            const V x = *reinterpret_cast<lds_v*>((size_t)((((k >> 9) << 9) + (threadIdx.x & 15)) << SHB));
+#else
+            const V x = *reinterpret_cast<lds_v*>((size_t)(k << SHB));
+#endif
 #pragma unroll
             for (int c = 0; c < CB; ++c) t[c] = x[c];
           } else {
             const unsigned hw = up ? wd >> 16 : wd;
             const unsigned k = __builtin_amdgcn_ubfe(hw, 0, 15);
             sg = (hw & 0x8000u) ? (real)-1 : (real)1;
-            vload<real, CB>(ts + ((size_t)(q * 4 + s4) * M + k) * CB, t);
+            vload<real, CB>(ts + (size_t)k * CB, t);
           }
 #pragma unroll
           for (int c = 0; c < CB; ++c) acc[c] = fma(t[c], sg, acc[c]);
@@ -3295,6 +3311,7 @@ struct sa_ctx {
   bool big = false;
   uint32_t* d_inv32 = nullptr;
   uint16_t* d_invb = nullptr;  // k_secb's bank-aware bucket table (build_invb), built on first batched use
+  uint16_t* d_fwdb = nullptr;  // k_secb's Ab table, bank-aware step order per row (build_fwdb), the same
   bool invb_done = false;
   uint16_t* d_fwd = nullptr;
   uint32_t* d_fwd2 = nullptr;
@@ -3577,7 +3594,8 @@ int download(sa_ctx* c, double* dst, const void* src, size_t count) {
 template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
-  a.inv = c->d_inv; a.inv32 = c->d_inv32; a.invb = c->d_invb; a.fwd = (const ushort4*)c->d_fwd; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
+  a.inv = c->d_inv; a.inv32 = c->d_inv32; a.invb = c->d_invb; a.fwd = (const ushort4*)c->d_fwd;
+  a.fwdb = (const ushort4*)c->d_fwdb; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
   a.tau = (real*)c->d_tau; a.iters = c->d_iters;
@@ -4541,9 +4559,143 @@ int build_banked(sa_ctx* c, const std::vector<int>& sets, int gsize, int nbank, 
 
 bool banks_enabled(const sa_ctx* c) { return !(c->plan & SA_PLAN_NO_BANKS); }
 
+// ---- bank-aware Ab row order ----------------------------------------------
+// k_secb's Ab pass gives lane L of a wave row r0 + L and reads, per step, one
+// staged T element (section s, column k(r, s)) per lane: for 16-byte T rows a
+// ds_read_b128 whose four 16-lane groups each take one LDS cycle per distinct
+// row on their busiest 16-byte bank group (MI355X_MICROARCH.md §LDS).  In
+// section order the columns k(r, s) of 16 rows are random: ~3 cycles per
+// group.  A row's partial sum does not care in which order its W sections
+// are added, so each row gets its own step order: a local search over swaps
+// of two steps of one row that lowers, per lane group, the largest number of
+// rows on one bank in a step (the addition order changes, the terms do not).
+// Rows n .. npad-1 (the last block's idle lanes) repeat a real row of their
+// lane group (a broadcast); sections past L read column 0 (a broadcast).
+void fwdb_group(const sa_ctx* c, int g, const uint16_t* fwd, int npad, uint16_t* out) {
+  const int W = c->WB, M = c->M, n = c->n, L = c->L;
+  const int rowb = c->CB * (int)rsz(c);  // bytes per staged T element
+  const bool b128 = rowb == 16;
+  const int gsize = b128 ? 16 : 32, nbank = b128 ? 16 : 32, ngroups = 64 / gsize;
+  const bool search = banks_enabled(c);
+  std::mt19937 rng(0xab0000u + (uint32_t)g);
+  std::vector<int> cnt((size_t)W * nbank), perm((size_t)gsize * W), bank((size_t)gsize * W), cost(W);
+  std::vector<uint16_t> ent((size_t)gsize * W);
+  auto step_cost = [&](int st) {
+    int mx = 0;
+    for (int b = 0; b < nbank; ++b) mx = std::max(mx, cnt[(size_t)st * nbank + b]);
+    return mx;
+  };
+  for (int b0 = 0; b0 < npad; b0 += 64) {
+    for (int G = 0; G < ngroups; ++G) {
+      int rows[32], nreal = 0;
+      for (int j = 0; j < gsize; ++j) {
+        const int lane = b128 ? kLdsGroups16[G][j] : G * 32 + j;
+        rows[j] = b0 + lane;
+      }
+      // entries (s * M + k | sign) and banks of the real rows, identity order
+      std::fill(cnt.begin(), cnt.end(), 0);
+      for (int j = 0; j < gsize; ++j) {
+        const int r = rows[j];
+        if (r >= n) continue;
+        ++nreal;
+        for (int sl = 0; sl < W; ++sl) {
+          const int l = g * W + sl;
+          uint16_t e = 0;
+          if (l < L) e = fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)];
+          const unsigned k = e & 0x7fffu;
+          ent[(size_t)j * W + sl] = (uint16_t)(((unsigned)sl * M + k) | (e & 0x8000u));
+          bank[(size_t)j * W + sl] = l < L ? (int)(((unsigned)sl * M + k) % (unsigned)nbank) : -1;
+          perm[(size_t)j * W + sl] = sl;
+          if (l < L) ++cnt[(size_t)sl * nbank + bank[(size_t)j * W + sl]];
+        }
+      }
+      if (search && nreal > 1) {
+        for (int st = 0; st < W; ++st) cost[st] = step_cost(st);
+        for (int it = 0; it < 64 * W; ++it) {
+          int s1 = 0;
+          for (int st = 1; st < W; ++st)
+            if (cost[st] > cost[s1]) s1 = st;
+          if (cost[s1] <= 1) break;
+          int bm = 0;
+          for (int b = 1; b < nbank; ++b)
+            if (cnt[(size_t)s1 * nbank + b] > cnt[(size_t)s1 * nbank + bm]) bm = b;
+          int cand[32], nc = 0;
+          for (int j = 0; j < gsize; ++j)
+            if (rows[j] < n && bank[(size_t)j * W + perm[(size_t)j * W + s1]] == bm) cand[nc++] = j;
+          if (nc == 0) break;
+          const int j = cand[rng() % (unsigned)nc];
+          const int s2 = (int)(rng() % (unsigned)W);
+          if (s2 == s1) continue;
+          int& x = perm[(size_t)j * W + s1];
+          int& y = perm[(size_t)j * W + s2];
+          const int bx = bank[(size_t)j * W + x], by = bank[(size_t)j * W + y];
+          auto mv = [&](int st, int b, int d) {
+            if (b >= 0) cnt[(size_t)st * nbank + b] += d;
+          };
+          mv(s1, bx, -1); mv(s2, by, -1); mv(s1, by, +1); mv(s2, bx, +1);
+          const int n1 = step_cost(s1), n2 = step_cost(s2);
+          if (n1 + n2 <= cost[s1] + cost[s2]) {
+            std::swap(x, y);
+            cost[s1] = n1;
+            cost[s2] = n2;
+          } else {
+            mv(s1, by, -1); mv(s2, bx, -1); mv(s1, bx, +1); mv(s2, by, +1);
+          }
+        }
+      }
+      // out [g * W/4 + q][npad][4]: step st = 4 q + slot; idle rows copy the
+      // group's first real row (or, with none, row 0 of the block's order)
+      int jr = -1;
+      for (int j = 0; j < gsize && jr < 0; ++j)
+        if (rows[j] < n) jr = j;
+      for (int j = 0; j < gsize; ++j) {
+        const int src = rows[j] < n ? j : jr;
+        for (int st = 0; st < W; ++st) {
+          const uint16_t e = src >= 0 ? ent[(size_t)src * W + perm[(size_t)src * W + st]] : (uint16_t)((unsigned)st * M);
+          out[((size_t)(g * (W / 4) + st / 4) * npad + rows[j]) * 4 + (st % 4)] = e;
+        }
+      }
+    }
+  }
+}
+
+int build_fwdb(sa_ctx* c) {
+  const int n = c->n, npad = (n + 63) & ~63, Gb = c->Gb, W = c->WB;
+  // the host copy of d_fwd, [G][n][4] (built again from the ordering: the
+  // same entries build_tables uploads)
+  const int lgM = ilog2(c->M);
+  const int G = (c->L + kSG - 1) / kSG * (kSG / kSpw);
+  std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);
+  for (int l = 0; l < c->L; ++l)
+    for (int r = 0; r < n; ++r) {
+      const uint32_t v = c->ordering[(size_t)l * n + r];
+      fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)] =
+          (uint16_t)((v & (uint32_t)(c->M - 1)) | ((__builtin_popcount(v >> lgM) & 1u) << 15));
+    }
+  std::vector<uint16_t> out((size_t)Gb * W * npad, 0);
+  unsigned nth = std::thread::hardware_concurrency();
+  nth = nth == 0 ? 1 : (nth > 16 ? 16 : nth);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nth; ++t)
+    th.emplace_back([&, t]() {
+      for (int g = (int)t; g < Gb; g += (int)nth) fwdb_group(c, g, fwd.data(), npad, out.data());
+    });
+  for (auto& x : th) x.join();
+  int rc = dev_alloc(c, (void**)&c->d_fwdb, out.size() * 2);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_fwdb, out.data(), out.size() * 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return SA_OK;
+}
+
 // k_secb (16-byte rows: binary32 CB = 4, binary64 CB = 2; E >= 4): lane L of a
 // wave holds columns elem_index<E>(L ^ 3 in binary32, i) (quad-mirrored positions)
 int ensure_invb(sa_ctx* c) {
+  // the Ab table first (every k_secb configuration reads it)
+  if (c->backend == SA_BACKEND_HADAMARD && c->CB > 0 && !c->big && !c->d_fwdb) {
+    if (c->WB * c->M >= 32768) return fail(SA_ERR_UNSUPPORTED, "k_secb: W * M >= 2^15");
+    if (int rc = build_fwdb(c)) return rc;
+  }
   if (c->invb_done) return SA_OK;
   c->invb_done = true;
   if (!(banks_enabled(c) && c->backend == SA_BACKEND_HADAMARD && c->CB > 0 && c->CB * (int)rsz(c) == 16 &&
@@ -5183,6 +5335,7 @@ void sa_destroy(sa_ctx* c) {
   dev_free(c->d_inv);
   dev_free(c->d_inv32);
   dev_free(c->d_invb);
+  dev_free(c->d_fwdb);
   dev_free(c->d_fwd);
   dev_free(c->d_fwd2);
   dev_free(c->d_fwd3);

@@ -506,6 +506,84 @@ __device__ __forceinline__ void fwht_wave_sgn(float (&x)[E], float s1, float s2)
   bfly_swap<32, float, E>(x);
 }
 
+// fwht_wave_sgn of two sections' values at once (binary32): each DPP stage is
+// one asm block over four registers of x and y (one pair of wait states per
+// block instead of per two registers, and four independent ops between a
+// register's write and its next DPP read); the same operations on every
+// register, so the same bits as two fwht_wave_sgn calls.
+__device__ __forceinline__ void quad_fmac4(float& a, float& b, float& c, float& d, float s1, float s2) {
+  asm("s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %0, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %1, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %2, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %3, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %0, %5 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %1, %5 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %2, %5 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %3, %5 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1"
+      : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+      : "v"(s1), "v"(s2));
+}
+template <int m>
+__device__ __forceinline__ void bank_bfly4(float& a, float& b, float& c, float& d) {
+  static_assert(m == 4 || m == 8, "bank butterfly");
+  float r0, r1, r2, r3;
+  if constexpr (m == 4)
+    asm("s_nop 1\n\t"
+        "v_add_f32_dpp %0, %4, %4 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_add_f32_dpp %1, %5, %5 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_add_f32_dpp %2, %6, %6 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_add_f32_dpp %3, %7, %7 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+        "v_sub_f32_dpp %0, %4, %4 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+        "v_sub_f32_dpp %1, %5, %5 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+        "v_sub_f32_dpp %2, %6, %6 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+        "v_sub_f32_dpp %3, %7, %7 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+        "s_nop 1"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(a), "v"(b), "v"(c), "v"(d));
+  else
+    asm("s_nop 1\n\t"
+        "v_add_f32_dpp %0, %4, %4 row_shl:8 row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %1, %5, %5 row_shl:8 row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %2, %6, %6 row_shl:8 row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %3, %7, %7 row_shl:8 row_mask:0xf bank_mask:0x3\n\t"
+        "v_sub_f32_dpp %0, %4, %4 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+        "v_sub_f32_dpp %1, %5, %5 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+        "v_sub_f32_dpp %2, %6, %6 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+        "v_sub_f32_dpp %3, %7, %7 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+        "s_nop 1"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3) : "v"(a), "v"(b), "v"(c), "v"(d));
+  a = r0; b = r1; c = r2; d = r3;
+}
+template <int E>
+__device__ __forceinline__ void fwht_wave_sgn_pair(float (&x)[E], float (&y)[E], float s1, float s2) {
+  static_assert(E >= 2 && E % 2 == 0, "pairs of elements");
+#pragma unroll
+  for (int h = 1; h < E; h <<= 1) {
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (!(i & h)) {
+        const float a = x[i], b = x[i | h];
+        x[i] = a + b;
+        x[i | h] = a - b;
+        const float c = y[i], d = y[i | h];
+        y[i] = c + d;
+        y[i | h] = c - d;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < E; i += 2) quad_fmac4(x[i], x[i + 1], y[i], y[i + 1], s1, s2);
+#pragma unroll
+  for (int i = 0; i < E; i += 2) bank_bfly4<4>(x[i], x[i + 1], y[i], y[i + 1]);
+#pragma unroll
+  for (int i = 0; i < E; i += 2) bank_bfly4<8>(x[i], x[i + 1], y[i], y[i + 1]);
+  bfly_swap<16, float, E>(x);
+  bfly_swap<16, float, E>(y);
+  bfly_swap<32, float, E>(x);
+  bfly_swap<32, float, E>(y);
+}
+
 template <typename real> __device__ __forceinline__ real dsqrt(real x);
 template <> __device__ __forceinline__ float dsqrt<float>(float x) { return sqrtf(x); }
 template <> __device__ __forceinline__ double dsqrt<double>(double x) { return sqrt(x); }
@@ -1985,6 +2063,11 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 //                  extra round trip after tau)
 //   SA_GSIGN       the gather's sign a constant of each half of the bank-aware
 //                  step order (two loops) instead of selected per step
+//   SA_F32_KH      binary32 (CB = 4 or E = 16) bucket h-steps in flight
+//   SA_F32_LATE_F / SA_F32_LATE_B  binary32 (CB = 4): the Ab-table rows / the
+//                  previous estimate after the gather (C3 +1.5 %, C4 neutral;
+//                  with the freed registers a third table buffer (loads two
+//                  blocks ahead) measured -2 %, KH = 4 -5 %: spills)
 // Round 5, interleaved A/B x2: binary32 C3 14.55 k -> 14.96 k, C4 6.93 k ->
 // 7.12 k cw/s (SA_GSIGN); binary64 C3 7.03 k -> 7.33 k, C4 3.22 k -> 3.36 k
 // (all three; SA_GSIGN alone 7.21 k / 3.32 k); then LATE_B with KH = 2: C3
@@ -2004,6 +2087,19 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 #ifndef SA_F64_LATE_B
 #define SA_F64_LATE_B 1
 #endif
+#ifndef SA_F32_KH
+#define SA_F32_KH 2
+#endif
+//   SA_FWHT_PAIR   binary32: the section transforms of codeword pairs interleaved
+#ifndef SA_FWHT_PAIR
+#define SA_FWHT_PAIR 1
+#endif
+#ifndef SA_F32_LATE_F
+#define SA_F32_LATE_F 1
+#endif
+#ifndef SA_F32_LATE_B
+#define SA_F32_LATE_B 1
+#endif
 template <typename real, int E, int CB, int W, bool ZIL = false>
 __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2012,12 +2108,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // binary64: fewer loads in flight so a wave fits 128 VGPRs (two workgroups per CU)
   constexpr bool F64 = sizeof(real) == 8;
   // bucket h-steps with table loads in flight together (binary64: SA_F64_KH)
-  constexpr int KH = F64 ? SA_F64_KH : ((E >= 16 || CB >= 4) ? 2 : 4);
+  constexpr int KH = F64 ? SA_F64_KH : ((E >= 16 || CB >= 4) ? SA_F32_KH : 4);
   // binary64: the first Ab-table rows loaded after the gather instead of with
   // the first loads (their registers are then free for the table stream)
-  constexpr bool LATE_F = F64 && SA_F64_LATE_F;
+  constexpr bool LATE_F = F64 ? SA_F64_LATE_F : SA_F32_LATE_F;
   // binary64: the previous estimate of codeword 0 loaded after the gather too
-  constexpr bool LATE_B = F64 && SA_F64_LATE_B;
+  constexpr bool LATE_B = (F64 ? SA_F64_LATE_B : SA_F32_LATE_B) && !(CB <= 2 && !F64);
   // rows per thread whose Ab-table loads are in flight together (one with 16
   // sections at CB = 4: their 4 table words per row already fill the registers)
   constexpr int KR = (CB >= 4 || F64) ? (W > 8 && (CB >= 4 || F64) ? 1 : 2) : 3;
@@ -2143,12 +2239,15 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // binary32: a workgroup-uniform base + this wave's 32-bit offset (SGPR-base
   // loads; binary64 keeps the per-wave pointer, its scratch grew otherwise)
   const uint16_t* il = (banked ? a.invb : a.inv) + (size_t)lc * a.w;
+  auto load_tb = [&](int h0, ushort4 (&dst)[KH][NQ]) {
+    if constexpr (F64)
+      load_buckets<E, KH>(il, h0, a.nhi, M, lpos, dst);
+    else
+      load_buckets_off<E, KH>((banked ? a.invb : a.inv) + (size_t)g * W * a.w, (unsigned)((lc - g * W) * a.w), h0,
+                              a.nhi, M, lpos, dst);
+  };
   ushort4 tb[KH][NQ];
-  if constexpr (F64)
-    load_buckets<E, KH>(il, 0, a.nhi, M, lpos, tb);
-  else
-    load_buckets_off<E, KH>((banked ? a.invb : a.inv) + (size_t)g * W * a.w, (unsigned)((lc - g * W) * a.w), 0,
-                            a.nhi, M, lpos, tb);
+  load_tb(0, tb);
   // previous beta: all CB codewords up front when registers allow (CB <= 2),
   // else codeword 0 now and codeword c+1 while c is denoised (PB false)
   real bprev[PB ? CB : 2][E];
@@ -2233,13 +2332,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     auto block = [&](int h0, int sgf) {
       ushort4 tn[KH][NQ];
       const bool more = h0 + KH < a.nhi;
-      if (more) {
-        if constexpr (F64)
-          load_buckets<E, KH>(il, h0 + KH, a.nhi, M, lpos, tn);
-        else
-          load_buckets_off<E, KH>((banked ? a.invb : a.inv) + (size_t)g * W * a.w, (unsigned)((lc - g * W) * a.w),
-                                  h0 + KH, a.nhi, M, lpos, tn);
-      }
+      if (more) load_tb(h0 + KH, tn);
 #pragma unroll
       for (int hh = 0; hh < KH; ++hh) {
         if (h0 + hh < a.nhi) {
@@ -2292,6 +2385,15 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     if constexpr (SGN) fwht_wave_sgn<E>(x, s1, s2);
     else fwht_wave<real, E>(x, lane, ml);
   };
+  // binary32 codeword pairs: the two transforms of a pair interleaved
+  constexpr bool FP = SA_FWHT_PAIR && SGN && CB % 2 == 0 && E >= 2;
+  auto fwht_all = [&]() {
+    if constexpr (FP) {
+#pragma unroll
+      for (int c = 0; c < CB; c += 2) fwht_wave_sgn_pair<E>(v[c], v[c + 1], s1, s2);
+    }
+  };
+  fwht_all();
   const real inv_sn = (real)1 / a.sqrt_n;
   real bbl[CB], mx[CB], S[CB], S2[CB];
 #pragma unroll
@@ -2300,7 +2402,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       if (c + 1 < CB)
         load_section_nt<real, E>(a.beta + (size_t)bc[c + 1] * LM + (size_t)lc * M, bprev[(c + 1) & 1], lpos, M);
     }
-    fwht_sec(v[c]);
+    if constexpr (!FP) fwht_sec(v[c]);
     const real k = cl[c] / tau2[c];
     real m = neg_inf<real>();
 #pragma unroll
@@ -2337,13 +2439,14 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     if (have && live[c]) store_section_nt<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, v[c], lpos, M);
     if (have) {
       bbl[c] = S2[c] * scale * scale;
-      fwht_sec(v[c]);  // T_l = H_M beta_l (natural positions)
+      if constexpr (!FP) fwht_sec(v[c]);  // T_l = H_M beta_l (natural positions)
     } else {
       bbl[c] = 0;
 #pragma unroll
       for (int i = 0; i < E; ++i) v[c][i] = 0;
     }
   }
+  if (have) fwht_all();  // (FP) the T transforms of the codeword pairs
   STAMP(4);
   __syncthreads();  // every wave is done with z before T overwrites it
 #pragma unroll

@@ -860,8 +860,9 @@ struct SecArgs {
   const uint16_t* __restrict__ invb;
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   // k_secb's Ab table (build_fwdb): [Gb * W / 4][npad][4] with npad = n rounded
-  // up to 64; entry (s * M + k) | sign << 15 for the workgroup's local section
-  // s, each row's W entries in a bank-aware step order
+  // up to 64; entry (s * M + t_pos(k)) | sign << 15 for the workgroup's local
+  // section s (t_pos: the staged image's position of column k), each row's W
+  // entries in a bank-aware step order
   const ushort4* __restrict__ fwdb;
   const uint32_t* __restrict__ fwd2; // [ceil(L/2)][n] the same entries of one section pair (k_sec2)
   const uint32_t* __restrict__ fwd3; // [ceil(L/3)][n] a section triple, 10-bit fields k | sign<<9 (M <= 512)
@@ -2456,7 +2457,11 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       real o[CB];
 #pragma unroll
       for (int c = 0; c < CB; ++c) o[c] = v[c][i];
-      vstore<real, CB>(ts + ((size_t)wv * M + e) * CB, o);
+      // staged at t_pos(e): consecutive lanes write consecutive rows (in
+      // natural order a lane's Q elements are adjacent, and the store of one
+      // register by 64 lanes has a Q-row stride: a Q-way bank conflict)
+      constexpr int Q = E < 4 ? E : 4;
+      vstore<real, CB>(ts + ((size_t)wv * M + (i / Q) * 64 * Q + (i % Q) * 64 + lane) * CB, o);
     }
   }
   if (lane == 0) {
@@ -4674,6 +4679,15 @@ bool banks_enabled(const sa_ctx* c) { return !(c->plan & SA_PLAN_NO_BANKS); }
 // rows on one bank in a step (the addition order changes, the terms do not).
 // Rows n .. npad-1 (the last block's idle lanes) repeat a real row of their
 // lane group (a broadcast); sections past L read column 0 (a broadcast).
+// LDS position of T column e in k_secb's staged image: the element index of
+// (lane, register i) is (i / Q) 64 Q + lane Q + i % Q (elem_index), staged at
+// (i / Q) 64 Q + (i % Q) 64 + lane
+unsigned t_pos(int E, unsigned e) {
+  const unsigned Q = E < 4 ? (unsigned)E : 4u;
+  const unsigned blk = e / (64 * Q), rem = e % (64 * Q);
+  return blk * 64 * Q + (rem % Q) * 64 + rem / Q;
+}
+
 void fwdb_group(const sa_ctx* c, int g, const uint16_t* fwd, int npad, uint16_t* out) {
   const int W = c->WB, M = c->M, n = c->n, L = c->L;
   const int rowb = c->CB * (int)rsz(c);  // bytes per staged T element
@@ -4705,7 +4719,7 @@ void fwdb_group(const sa_ctx* c, int g, const uint16_t* fwd, int npad, uint16_t*
           const int l = g * W + sl;
           uint16_t e = 0;
           if (l < L) e = fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)];
-          const unsigned k = e & 0x7fffu;
+          const unsigned k = t_pos(c->E, e & 0x7fffu);
           ent[(size_t)j * W + sl] = (uint16_t)(((unsigned)sl * M + k) | (e & 0x8000u));
           bank[(size_t)j * W + sl] = l < L ? (int)(((unsigned)sl * M + k) % (unsigned)nbank) : -1;
           perm[(size_t)j * W + sl] = sl;

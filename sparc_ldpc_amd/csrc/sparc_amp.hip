@@ -2092,6 +2092,9 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 #define SA_F32_KH 2
 #endif
 //   SA_FWHT_PAIR   binary32: the section transforms of codeword pairs interleaved
+#ifndef SA_ROWC_U12
+#define SA_ROWC_U12 1
+#endif
 #ifndef SA_FWHT_PAIR
 #define SA_FWHT_PAIR 1
 #endif
@@ -2738,7 +2741,7 @@ __global__ void __launch_bounds__(256) k_rowv(RowArgs<real> a) {
 // Onsager residual (sparc_ldpc.py:220), stores z [NC][n][CB] as one 16-byte
 // vector per row, and the z^2 partial of each codeword's block.  A stopped
 // codeword keeps its z and z^2 partials.
-template <typename real, int CB>
+template <typename real, int CB, int U = 8>
 __global__ void __launch_bounds__(256) k_rowc(RowArgs<real> a, int pil) {
   using V = real __attribute__((ext_vector_type(CB)));
   constexpr int RPL = 2;  // rows per lane
@@ -2788,7 +2791,6 @@ __global__ void __launch_bounds__(256) k_rowc(RowArgs<real> a, int pil) {
     const int gq = (a.G + 3) / 4, g0 = wv * gq, g1 = min(a.G, g0 + gq);
     V acc[RPL] = {};
     if (pil) {
-      constexpr int U = 8;
       const V* p = reinterpret_cast<const V*>(a.abp) + (size_t)chunk * a.G * n;
       for (int gg = g0; gg < g1; gg += U) {
         V t[RPL][U];
@@ -3950,7 +3952,11 @@ int launch_row(sa_ctx* c, int B, int mode, int t, int es, int G, int Gb, int pt 
   if (c->row_kind == 5 && mode != ROW_ABOUT) {
     constexpr int CBz = 16 / (int)sizeof(real);  // codewords per 16-byte row
     a.Bc = B;
-    plaunch(c, k_rowc<real, CBz>, dim3(c->NZ2, (B + CBz - 1) / CBz), 256, 0, a, mode == ROW_AMP ? 1 : 0);
+    // each wave's G / 4 partials in one batch of loads (U = 12: C4's 48 groups)
+    if (SA_ROWC_U12 && (a.G + 3) / 4 > 8 && (a.G + 3) / 4 <= 12)
+      plaunch(c, k_rowc<real, CBz, 12>, dim3(c->NZ2, (B + CBz - 1) / CBz), 256, 0, a, mode == ROW_AMP ? 1 : 0);
+    else
+      plaunch(c, k_rowc<real, CBz>, dim3(c->NZ2, (B + CBz - 1) / CBz), 256, 0, a, mode == ROW_AMP ? 1 : 0);
   } else if (c->row_kind == 5) {  // A beta out of k_sec's [B][G][n] partials (sa_Ab after a batched decode)
     plaunch(c, k_row<real, 4>, dim3(c->NZ, B), 4 * 64, 0, a);
   } else if (c->row_kind == 1) {

@@ -118,6 +118,13 @@ int sa_create_matrix_random(sa_ctx** out, int L, int M, int n, uint64_t seed, do
  * ldpc/amp_exit.py:113-116): a new context over the given parent sections. */
 int sa_subset(const sa_ctx* parent, const int64_t* sections, int Ls, sa_ctx** out);
 
+/* A second context over src's operator (the same L, M, n, ordering, backend,
+ * precision, device and plan) that shares src's device tables, read-only,
+ * and has its own stream, workspace and power allocation: concurrent decodes
+ * of one operator (joint.JointPipeline's slices) read one copy of the tables
+ * from L2.  src must outlive the twin.  Hadamard backend only. */
+int sa_create_twin(sa_ctx* src, sa_ctx** out);
+
 void sa_destroy(sa_ctx* ctx);
 
 /* Replaces the Ab closure, sparc_ldpc.py:143-144 (-> block_sub_fht.Ax

@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0)
     ap.add_argument("--no-ref", action="store_true", help="skip the one-decoder reference decode (traces)")
+    ap.add_argument("--no-twin", action="store_true",
+                    help="the pipeline's slices build their own operator tables (A/B of SparcOperator.twin)")
     ap.add_argument("--parts", type=int, default=2,
                     help="concurrent slices of the batch, each on its own streams (joint.JointPipeline); 1: one decoder")
     args = ap.parse_args()
@@ -156,6 +158,7 @@ def main():
     # step must reproduce rep for rep
     jd.stage(idx, noise, Pl)
     ref = None if args.no_ref else jd.decode_staged(idx, Pl, "soft", args.soft_iter)
+    joint.TWIN_SLICES = not args.no_twin
     runner = joint.joint_pipeline(jd, args.parts) if args.parts > 1 else jd
     runner.stage(idx, noise, Pl)
 

@@ -61,7 +61,7 @@ def plan_bits(plan) -> int:
 
 # Every symbol include/sparc_amp.h declares (tests check the export table).
 EXPORTS = (
-    "sa_create", "sa_create_ex", "sa_create_matrix", "sa_create_matrix_random", "sa_subset", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
+    "sa_create", "sa_create_ex", "sa_create_matrix", "sa_create_matrix_random", "sa_subset", "sa_create_twin", "sa_destroy", "sa_Ab", "sa_Az", "sa_amp",
     "sa_reserve", "sa_stage", "sa_stage_power_batch", "sa_run", "sa_wait", "sa_fetch", "sa_fetch_z", "sa_run_event_ms",
     "sa_profile", "sa_profile_rep", "sa_profile_dispatch", "sa_profile_kinds", "sa_decide",
     "sa_decide_async", "sa_decide_collect", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
@@ -79,6 +79,7 @@ _SIG = {
     "sa_create_matrix": (_I, [ct.POINTER(_P), _I, _I, _I, _D, _I, _I]),
     "sa_create_matrix_random": (_I, [ct.POINTER(_P), _I, _I, _I, ct.c_uint64, ct.c_double, _I, _I]),
     "sa_subset": (_I, [_P, ct.POINTER(ct.c_int64), _I, ct.POINTER(_P)]),
+    "sa_create_twin": (_I, [_P, ct.POINTER(_P)]),
     "sa_destroy": (None, [_P]),
     "sa_Ab": (_I, [_P, _I, _D, _D]),
     "sa_Az": (_I, [_P, _I, _D, _D]),

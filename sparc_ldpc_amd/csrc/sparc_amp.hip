@@ -3422,6 +3422,7 @@ struct sa_ctx {
   uint32_t* d_inv32 = nullptr;
   uint16_t* d_invb = nullptr;  // k_secb's bank-aware bucket table (build_invb), built on first batched use
   uint16_t* d_fwdb = nullptr;  // k_secb's Ab table, bank-aware step order per row (build_fwdb), the same
+  bool borrowed = false;       // the operator tables are another context's (sa_create_twin): not freed here
   bool invb_done = false;
   uint16_t* d_fwd = nullptr;
   uint32_t* d_fwd2 = nullptr;
@@ -4936,7 +4937,7 @@ int set_lds_limits() {
 }
 
 int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int backend, int prec,
-                int device, int plan) {
+                int device, int plan, const sa_ctx* share = nullptr) {
   if (!out) return fail(SA_ERR_ARG, "out is NULL");
   *out = nullptr;
   if (L <= 0 || M <= 0 || n <= 0) return fail(SA_ERR_ARG, "L, M, n must be positive");
@@ -5113,6 +5114,11 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       hipError_t e = hipMemsetAsync(c->d_A, 0, (size_t)c->np * c->lda * s, c->stream);
       if (e != hipSuccess) rc = fail(SA_ERR_HIP, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
     }
+  } else if (share) {  // sa_create_twin: the same tables, read-only, borrowed
+    c->d_inv = share->d_inv; c->d_inv32 = share->d_inv32; c->d_invb = share->d_invb;
+    c->d_fwdb = share->d_fwdb; c->d_fwd = share->d_fwd; c->d_fwd2 = share->d_fwd2; c->d_fwd3 = share->d_fwd3;
+    c->invb_done = share->invb_done;
+    c->borrowed = true;
   } else {
     rc = build_tables(c);
   }
@@ -5449,19 +5455,34 @@ int sa_subset(const sa_ctx* parent, const int64_t* sections, int Ls, sa_ctx** ou
                      parent->plan);
 }
 
+int sa_create_twin(sa_ctx* src, sa_ctx** out) {
+  if (!out) return fail(SA_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (check_ctx(src)) return SA_ERR_ARG;
+  if (src->backend != SA_BACKEND_HADAMARD)
+    return fail(SA_ERR_UNSUPPORTED, "sa_create_twin: Hadamard-backend contexts only");
+  HIP_TRY(hipSetDevice(src->device));
+  // the lazily built batched-kernel tables first, so that both contexts use them
+  if (int rc = ensure_invb(src)) return rc;
+  return create_impl(out, src->L, src->M, src->n, src->ordering.data(), src->backend, src->prec, src->device,
+                     src->plan, src);
+}
+
 void sa_destroy(sa_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   drop_graphs(c);
   free_workspace(c);
-  dev_free(c->d_inv);
-  dev_free(c->d_inv32);
-  dev_free(c->d_invb);
-  dev_free(c->d_fwdb);
-  dev_free(c->d_fwd);
-  dev_free(c->d_fwd2);
-  dev_free(c->d_fwd3);
+  if (!c->borrowed) {
+    dev_free(c->d_inv);
+    dev_free(c->d_inv32);
+    dev_free(c->d_invb);
+    dev_free(c->d_fwdb);
+    dev_free(c->d_fwd);
+    dev_free(c->d_fwd2);
+    dev_free(c->d_fwd3);
+  }
   dev_free(c->d_A);
   dev_free(c->d_AT); dev_free(c->d_xz); dev_free(c->d_xb);
   dev_free(c->d_A8); dev_free(c->d_AT8); dev_free(c->d_zq); dev_free(c->d_bq);

@@ -103,7 +103,9 @@ class JointDecoder:
     """AMP operator + LDPC code + the shortened operator of the unprotected
     sections, for B-codeword batches of the joint schemes."""
 
-    def __init__(self, L, M, n, code, T, backend=None, precision=None, device=None, seed=0):
+    def __init__(self, L, M, n, code, T, backend=None, precision=None, device=None, seed=0, twin_of=None):
+        """twin_of: another JointDecoder whose operator tables this one shares
+        (SparcOperator.twin: own stream and workspace, one copy of the tables)."""
         self.L, self.M, self.n, self.T = int(L), int(M), int(n), int(T)
         self.logm = int(round(math.log2(M)))
         self.code = code
@@ -112,8 +114,12 @@ class JointDecoder:
         assert nl % self.logm == 0, "LDPC code must cover whole sections"
         self.ns = nl // self.logm
         self.l0 = self.L - self.ns
-        self.op = SparcOperator(L, M, n, make_ordering(L, M, n, seed), backend, precision, device)
-        self.sub = self.op.subset(np.arange(self.l0)) if self.l0 > 0 else None
+        if twin_of is not None and twin_of.op.backend == "hadamard":
+            self.op = twin_of.op.twin()
+            self.sub = twin_of.sub.twin() if twin_of.sub is not None else None
+        else:
+            self.op = SparcOperator(L, M, n, make_ordering(L, M, n, seed), backend, precision, device)
+            self.sub = self.op.subset(np.arange(self.l0)) if self.l0 > 0 else None
         self.total_bits = self.L * self.logm
         self.R = (self.L * self.logm - (code.N - code.K)) / n  # sparc_ldpc.py:541
         self._masked = None  # full-size operator for the per-codeword masked decodes (threshold mode)
@@ -280,7 +286,8 @@ class JointDecoder:
 
 class JointPipeline:
     """A batch of the joint decoder cut into `parts` consecutive slices, each
-    decoded by its own JointDecoder (its own operator context and HIP stream,
+    decoded by its own JointDecoder (its own operator context, sharing the first slice's
+    device tables (SparcOperator.twin), and HIP stream,
     its own LDPC context and stream) from its own host thread, so that one
     slice's belief-propagation tail (a few words on a few CUs for up to
     MAX_ITCOUNT iterations, c_ldpc.c:7) runs beside another slice's AMP
@@ -297,7 +304,8 @@ class JointPipeline:
         op, code = jd.op, jd.code
         for _ in range(int(parts) - 1):
             c2 = _ldpc.code(code.standard, code.rate, code.z, code.ptype, device=code._device)
-            self.parts.append(JointDecoder(jd.L, jd.M, jd.n, c2, jd.T, op.backend, op.precision, op.device))
+            self.parts.append(JointDecoder(jd.L, jd.M, jd.n, c2, jd.T, op.backend, op.precision, op.device,
+                                           twin_of=jd if TWIN_SLICES else None))
         self._pool = ThreadPoolExecutor(max_workers=len(self.parts), thread_name_prefix="joint")
         self._slices = None
 
@@ -358,6 +366,8 @@ _JP_CACHE: "dict[int, JointPipeline]" = {}
 
 # batches of at least this many codewords are decoded as two concurrent halves
 PIPELINE_MIN_BATCH = 64
+# the pipeline's extra slices share the first slice's operator tables
+TWIN_SLICES = True
 
 
 def joint_pipeline(jd: JointDecoder, parts=2) -> JointPipeline:

@@ -420,6 +420,22 @@ class SparcOperator:
         else:
             check(self._lib.sa_cancel_scaled(self._ctx, idx.shape[0], p, float(scale), dst.ctx))
 
+    def twin(self) -> "SparcOperator":
+        """A second operator context sharing this one's device tables
+        (sa_create_twin): its own stream and workspace for a concurrent
+        decode; keeps this operator alive."""
+        if self.backend != "hadamard":
+            raise ValueError("twin() needs a Hadamard-backend operator")
+        tw = SparcOperator.__new__(SparcOperator)
+        tw.L, tw.M, tw.n, tw.w = self.L, self.M, self.n, self.w
+        tw.backend, tw.precision, tw.device = self.backend, self.precision, self.device
+        tw.ordering, tw.plan_bits = self.ordering, self.plan_bits
+        tw._src = self  # the tables' owner outlives the twin
+        tw._ctx = _lib.ct.c_void_p()
+        check(self._lib.sa_create_twin(self._ctx, _lib.ct.byref(tw._ctx)))
+        tw._lib = self._lib
+        return tw
+
     def subset(self, sections) -> "SparcOperator":
         """Operator over the given parent sections (sparc_transforms_shorter)."""
         sec = np.ascontiguousarray(np.asarray(sections, dtype=np.int64).reshape(-1))

@@ -858,6 +858,8 @@ struct SecArgs {
   const uint16_t* __restrict__ inv;  // [L][w]  row of ordering value o, or n (zero slot)
   // k_secb: the bucket table in bank-aware step order (build_invb), or null
   const uint16_t* __restrict__ invb;
+  // the codeword-interleaved k_secb: invb (or inv) lane-major [L][nhi][64][E]
+  const uint16_t* __restrict__ invl;
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   // k_secb's Ab table (build_fwdb): [Gb * W / 4][npad][4] with npad = n rounded
   // up to 64; entry (s * M + t_pos(k)) | sign << 15 for the workgroup's local
@@ -2244,7 +2246,24 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   // loads; binary64 keeps the per-wave pointer, its scratch grew otherwise)
   const uint16_t* il = (banked ? a.invb : a.inv) + (size_t)lc * a.w;
   auto load_tb = [&](int h0, ushort4 (&dst)[KH][NQ]) {
-    if constexpr (F64)
+    if constexpr (ZIL && E % 4 == 0) {
+      // lane-major table: this lane's NQ quads of step h in one run of E * 2 bytes
+      const uint16_t* base = a.invl + (size_t)lc * a.nhi * 64 * E + (size_t)lane * E;
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh) {
+        const int h = h0 + hh < a.nhi ? h0 + hh : a.nhi - 1;
+#pragma unroll
+        for (int j = 0; j < NQ; j += 2) {
+          if (j + 1 < NQ) {
+            const uint4 q = *reinterpret_cast<const uint4*>(base + (size_t)h * 64 * E + 4 * j);
+            dst[hh][j] = *reinterpret_cast<const ushort4*>(&q.x);
+            dst[hh][j + 1] = *reinterpret_cast<const ushort4*>(&q.z);
+          } else {
+            dst[hh][j] = *reinterpret_cast<const ushort4*>(base + (size_t)h * 64 * E + 4 * j);
+          }
+        }
+      }
+    } else if constexpr (F64)
       load_buckets<E, KH>(il, h0, a.nhi, M, lpos, dst);
     else
       load_buckets_off<E, KH>((banked ? a.invb : a.inv) + (size_t)g * W * a.w, (unsigned)((lc - g * W) * a.w), h0,
@@ -3422,6 +3441,7 @@ struct sa_ctx {
   uint32_t* d_inv32 = nullptr;
   uint16_t* d_invb = nullptr;  // k_secb's bank-aware bucket table (build_invb), built on first batched use
   uint16_t* d_fwdb = nullptr;  // k_secb's Ab table, bank-aware step order per row (build_fwdb), the same
+  uint16_t* d_invl = nullptr;  // the codeword-interleaved k_secb's bucket table, lane-major (k_lane_major)
   bool borrowed = false;       // the operator tables are another context's (sa_create_twin): not freed here
   bool invb_done = false;
   uint16_t* d_fwd = nullptr;
@@ -3705,7 +3725,7 @@ int download(sa_ctx* c, double* dst, const void* src, size_t count) {
 template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
-  a.inv = c->d_inv; a.inv32 = c->d_inv32; a.invb = c->d_invb; a.fwd = (const ushort4*)c->d_fwd;
+  a.inv = c->d_inv; a.inv32 = c->d_inv32; a.invb = c->d_invb; a.invl = c->d_invl; a.fwd = (const ushort4*)c->d_fwd;
   a.fwdb = (const ushort4*)c->d_fwdb; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
@@ -4674,6 +4694,24 @@ int build_banked(sa_ctx* c, const std::vector<int>& sets, int gsize, int nbank, 
 
 bool banks_enabled(const sa_ctx* c) { return !(c->plan & SA_PLAN_NO_BANKS); }
 
+// [L][w] bucket table (slot h * M + column) -> [L][nhi][64][E]: lane L's E
+// entries of step h contiguous, in register order (columns elem_index<E >= 4>
+// of lane L ^ 3 in binary32 (sgn), of L in binary64)
+__global__ void k_lane_major(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, int L, int nhi, int M,
+                             int w, int E, int sgn) {
+  const size_t tot = (size_t)L * nhi * 64 * E;
+  for (size_t x = blockIdx.x * (size_t)blockDim.x + threadIdx.x; x < tot; x += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(x % E);
+    size_t t = x / E;
+    const int lane = (int)(t % 64);
+    t /= 64;
+    const int h = (int)(t % nhi), l = (int)(t / nhi);
+    const int lp = sgn ? (lane ^ 3) : lane;
+    const int e = (i / 4) * 256 + lp * 4 + (i % 4);
+    dst[x] = src[(size_t)l * w + (size_t)h * M + e];
+  }
+}
+
 // ---- bank-aware Ab row order ----------------------------------------------
 // k_secb's Ab pass gives lane L of a wave row r0 + L and reads, per step, one
 // staged T element (section s, column k(r, s)) per lane: for 16-byte T rows a
@@ -4822,18 +4860,30 @@ int ensure_invb(sa_ctx* c) {
   }
   if (c->invb_done) return SA_OK;
   c->invb_done = true;
-  if (!(banks_enabled(c) && c->backend == SA_BACKEND_HADAMARD && c->CB > 0 && c->CB * (int)rsz(c) == 16 &&
-        c->E >= 4 && c->nhi >= 2 && c->n + kInvbZeroRows <= 65535))
-    return SA_OK;
   const bool sgn = c->prec == SA_PREC_F32;  // k_secb's SGN (E >= 2)
-  std::vector<int> sets;
-  for (int i = 0; i < c->E; ++i)
-    for (int G = 0; G < 4; ++G)
-      for (int j = 0; j < 16; ++j) {
-        const int lane = kLdsGroups16[G][j], lp = sgn ? (lane ^ 3) : lane;
-        sets.push_back((i / 4) * 256 + lp * 4 + (i % 4));  // elem_index<E >= 4>
-      }
-  return build_banked(c, sets, 16, 16, &c->d_invb);
+  const bool rows16 = c->backend == SA_BACKEND_HADAMARD && c->CB > 0 && c->CB * (int)rsz(c) == 16 && !c->big;
+  if (rows16 && banks_enabled(c) && c->E >= 4 && c->nhi >= 2 && c->n + kInvbZeroRows <= 65535) {
+    std::vector<int> sets;
+    for (int i = 0; i < c->E; ++i)
+      for (int G = 0; G < 4; ++G)
+        for (int j = 0; j < 16; ++j) {
+          const int lane = kLdsGroups16[G][j], lp = sgn ? (lane ^ 3) : lane;
+          sets.push_back((i / 4) * 256 + lp * 4 + (i % 4));  // elem_index<E >= 4>
+        }
+    if (int rc = build_banked(c, sets, 16, 16, &c->d_invb)) return rc;
+  }
+  // the codeword-interleaved k_secb's copy of its bucket table with each
+  // lane's E entries of a step contiguous (one 16-byte load per lane and
+  // step at E = 8 instead of two 8-byte loads 512 B apart)
+  if (rows16 && c->E >= 4 && c->E % 4 == 0) {
+    const size_t cnt = (size_t)c->L * c->nhi * 64 * c->E;
+    if (int rc = dev_alloc(c, (void**)&c->d_invl, cnt * 2)) return rc;
+    k_lane_major<<<(int)std::min<size_t>((cnt + 255) / 256, 16384), 256, 0, c->stream>>>(
+        c->d_invb ? c->d_invb : c->d_inv, c->d_invl, c->L, c->nhi, c->M, c->w, c->E, sgn ? 1 : 0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  return SA_OK;
 }
 
 int build_dense(sa_ctx* c) {
@@ -5117,6 +5167,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   } else if (share) {  // sa_create_twin: the same tables, read-only, borrowed
     c->d_inv = share->d_inv; c->d_inv32 = share->d_inv32; c->d_invb = share->d_invb;
     c->d_fwdb = share->d_fwdb; c->d_fwd = share->d_fwd; c->d_fwd2 = share->d_fwd2; c->d_fwd3 = share->d_fwd3;
+    c->d_invl = share->d_invl;
     c->invb_done = share->invb_done;
     c->borrowed = true;
   } else {
@@ -5479,6 +5530,7 @@ void sa_destroy(sa_ctx* c) {
     dev_free(c->d_inv32);
     dev_free(c->d_invb);
     dev_free(c->d_fwdb);
+    dev_free(c->d_invl);
     dev_free(c->d_fwd);
     dev_free(c->d_fwd2);
     dev_free(c->d_fwd3);

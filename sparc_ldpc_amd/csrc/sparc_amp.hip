@@ -860,6 +860,8 @@ struct SecArgs {
   const uint16_t* __restrict__ invb;
   // the codeword-interleaved k_secb: invb (or inv) lane-major [L][nhi][64][E]
   const uint16_t* __restrict__ invl;
+  // [L] steps of invb's two halves that hold occupied slots (s0 | s1 << 16), or null
+  const uint32_t* __restrict__ hs;
   const ushort4* __restrict__ fwd;   // [G][n]  4 sections: (o & (M-1)) | parity(o >> log2 M) << 15
   // k_secb's Ab table (build_fwdb): [Gb * W / 4][npad][4] with npad = n rounded
   // up to 64; entry (s * M + t_pos(k)) | sign << 15 for the workgroup's local
@@ -2094,6 +2096,10 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 #define SA_F32_KH 2
 #endif
 //   SA_FWHT_PAIR   binary32: the section transforms of codeword pairs interleaved
+//   SA_SECB_COMPACT  the bank-aware halves' occupied slots in their first steps, the rest skipped
+#ifndef SA_SECB_COMPACT
+#define SA_SECB_COMPACT 1
+#endif
 #ifndef SA_ROWC_U12
 #define SA_ROWC_U12 1
 #endif
@@ -2352,10 +2358,11 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     constexpr int Q = E < 4 ? E : 4;
     // one block of KH h-steps; sgf >= 0: every step of the block has that
     // sign (the bank-aware order's halves), else sgn(h) per step
-    auto block = [&](int h0, int sgf) {
+    // hn: the next block's first step (< 0: none)
+    auto block = [&](int h0, int sgf, int hn) {
       ushort4 tn[KH][NQ];
-      const bool more = h0 + KH < a.nhi;
-      if (more) load_tb(h0 + KH, tn);
+      const bool more = hn >= 0;
+      if (more) load_tb(hn, tn);
 #pragma unroll
       for (int hh = 0; hh < KH; ++hh) {
         if (h0 + hh < a.nhi) {
@@ -2391,11 +2398,20 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     constexpr bool GS = SA_GSIGN && CB * sizeof(real) == 16 && E <= 8;
     if (GS && banked && half > 0 && half % KH == 0) {
       // the bank-aware order: the +1 steps, then the -1 steps; the sign is a
-      // constant of each loop (the same fmas with the same signs)
-      for (int h0 = 0; h0 < half; h0 += KH) block(h0, 0);
-      for (int h0 = half; h0 < a.nhi; h0 += KH) block(h0, 1);
+      // constant of each loop (the same fmas with the same signs).  Each half
+      // holds its occupied slots in its first s0 / s1 steps (build_invb: the
+      // section's largest column count, a multiple of KH): the rest, empty
+      // for every column, is skipped
+      int s0 = half, s1 = half;
+      if (a.hs) {
+        const unsigned v = a.hs[__builtin_amdgcn_readfirstlane(lc)];
+        s0 = (int)(v & 0xffffu);
+        s1 = (int)(v >> 16);
+      }
+      for (int h0 = 0; h0 < s0; h0 += KH) block(h0, 0, h0 + KH < s0 ? h0 + KH : (s1 > 0 ? half : -1));
+      for (int h0 = half; h0 < half + s1; h0 += KH) block(h0, 1, h0 + KH < half + s1 ? h0 + KH : -1);
     } else {
-      for (int h0 = 0; h0 < a.nhi; h0 += KH) block(h0, -1);
+      for (int h0 = 0; h0 < a.nhi; h0 += KH) block(h0, -1, h0 + KH < a.nhi ? h0 + KH : -1);
     }
   }
   if constexpr (LATE_F) load_f();
@@ -3442,6 +3458,7 @@ struct sa_ctx {
   uint16_t* d_invb = nullptr;  // k_secb's bank-aware bucket table (build_invb), built on first batched use
   uint16_t* d_fwdb = nullptr;  // k_secb's Ab table, bank-aware step order per row (build_fwdb), the same
   uint16_t* d_invl = nullptr;  // the codeword-interleaved k_secb's bucket table, lane-major (k_lane_major)
+  uint32_t* d_hs = nullptr;    // [L] occupied steps of d_invb's halves (build_banked)
   bool borrowed = false;       // the operator tables are another context's (sa_create_twin): not freed here
   bool invb_done = false;
   uint16_t* d_fwd = nullptr;
@@ -3725,7 +3742,8 @@ int download(sa_ctx* c, double* dst, const void* src, size_t count) {
 template <typename real>
 SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   SecArgs<real> a;
-  a.inv = c->d_inv; a.inv32 = c->d_inv32; a.invb = c->d_invb; a.invl = c->d_invl; a.fwd = (const ushort4*)c->d_fwd;
+  a.inv = c->d_inv; a.inv32 = c->d_inv32; a.invb = c->d_invb; a.invl = c->d_invl; a.hs = c->d_hs;
+  a.fwd = (const ushort4*)c->d_fwd;
   a.fwdb = (const ushort4*)c->d_fwdb; a.fwd2 = c->d_fwd2; a.fwd3 = c->d_fwd3; a.c = (const real*)c->d_c;
   a.z = (const real*)c->d_z; a.beta = (real*)c->d_beta; a.beta_out = (real*)c->d_beta; a.out = (real*)c->d_out;
   a.abp = (real*)c->d_abp; a.bbp = (real*)c->d_bbp; a.zzp = (const real*)c->d_zzp;
@@ -4588,11 +4606,24 @@ constexpr int kLdsGroups16[4][16] = {  // ds_read_b128
 // sets: nsets x gsize columns read by one lane group of one read
 // instruction; writes out[h * M + k] (h < nhi) for every column of the sets
 void banked_section(const sa_ctx* c, int l, const uint16_t* inv_l, uint16_t* out, const std::vector<int>& sets,
-                    int gsize, int nbank) {
-  const int M = c->M, n = c->n, S = c->nhi / 2;
+                    int gsize, int nbank, uint32_t* hs, int kh) {
+  const int M = c->M, n = c->n, Sh = c->nhi / 2;
   const int nsets = (int)sets.size() / gsize;
   std::mt19937 rng(0x5eed0000u + (uint32_t)l);
-  std::vector<int> A((size_t)gsize * S), cnt((size_t)S * nbank), emp(S), cost(S);
+  // per sign class, the section's largest number of occupied slots in one
+  // column (rounded up to whole blocks of kh steps): the steps used
+  int Sc[2] = {0, 0};
+  for (int cls = 0; cls < 2; ++cls) {
+    for (int col = 0; col < M; ++col) {
+      int m = 0;
+      for (int h = 0; h < c->nhi; ++h)
+        if ((__builtin_popcount(h) & 1) == cls && inv_l[(size_t)h * M + col] != (uint16_t)n) ++m;
+      Sc[cls] = std::max(Sc[cls], m);
+    }
+    Sc[cls] = std::min(Sh, std::max(kh, (Sc[cls] + kh - 1) / kh * kh));
+  }
+  if (hs) hs[l] = (uint32_t)Sc[0] | ((uint32_t)Sc[1] << 16);
+  std::vector<int> A((size_t)gsize * Sh), cnt((size_t)Sh * nbank), emp(Sh), cost(Sh);
   auto step_cost = [&](int st) {
     const int* ct = &cnt[(size_t)st * nbank];
     int mx = 0, mn = 1 << 30;
@@ -4606,6 +4637,7 @@ void banked_section(const sa_ctx* c, int l, const uint16_t* inv_l, uint16_t* out
   for (int si = 0; si < nsets; ++si) {
     const int* cols = &sets[(size_t)si * gsize];
     for (int cls = 0; cls < 2; ++cls) {
+      const int S = Sc[cls];
       std::fill(cnt.begin(), cnt.end(), 0);
       std::fill(emp.begin(), emp.end(), 0);
       for (int j = 0; j < gsize; ++j) {
@@ -4663,17 +4695,20 @@ void banked_section(const sa_ctx* c, int l, const uint16_t* inv_l, uint16_t* out
         const int zrow = n + ((zg - n % nbank + nbank) % nbank);  // the zero row on bank zg
         for (int j = 0; j < gsize; ++j) {
           const int v = A[(size_t)j * S + st];
-          out[(size_t)(cls * S + st) * M + cols[j]] = (uint16_t)(v >= 0 ? v : zrow);
+          out[(size_t)(cls * Sh + st) * M + cols[j]] = (uint16_t)(v >= 0 ? v : zrow);
         }
       }
+      for (int st = S; st < Sh; ++st)  // never gathered (every column's slots sit in the first S steps)
+        for (int j = 0; j < gsize; ++j) out[(size_t)(cls * Sh + st) * M + cols[j]] = (uint16_t)n;
     }
   }
 }
 
 // All sections in parallel on the host; uploaded into *dst.
-int build_banked(sa_ctx* c, const std::vector<int>& sets, int gsize, int nbank, uint16_t** dst) {
+int build_banked(sa_ctx* c, const std::vector<int>& sets, int gsize, int nbank, uint16_t** dst, int kh) {
   const int L = c->L, n = c->n, w = c->w;
   std::vector<uint16_t> inv((size_t)L * w, (uint16_t)n), out((size_t)L * w, 0);
+  std::vector<uint32_t> hs((size_t)L, 0);
   for (int l = 0; l < L; ++l)
     for (int r = 0; r < n; ++r) inv[(size_t)l * w + c->ordering[(size_t)l * n + r]] = (uint16_t)r;
   unsigned nth = std::thread::hardware_concurrency();
@@ -4682,12 +4717,15 @@ int build_banked(sa_ctx* c, const std::vector<int>& sets, int gsize, int nbank, 
   for (unsigned t = 0; t < nth; ++t)
     th.emplace_back([&, t]() {
       for (int l = (int)t; l < L; l += (int)nth)
-        banked_section(c, l, inv.data() + (size_t)l * w, out.data() + (size_t)l * w, sets, gsize, nbank);
+        banked_section(c, l, inv.data() + (size_t)l * w, out.data() + (size_t)l * w, sets, gsize, nbank,
+                       hs.data(), kh);
     });
   for (auto& x : th) x.join();
   int rc = dev_alloc(c, (void**)dst, out.size() * 2);
+  if (!rc) rc = dev_alloc(c, (void**)&c->d_hs, hs.size() * 4);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(*dst, out.data(), out.size() * 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->d_hs, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
@@ -4870,7 +4908,9 @@ int ensure_invb(sa_ctx* c) {
           const int lane = kLdsGroups16[G][j], lp = sgn ? (lane ^ 3) : lane;
           sets.push_back((i / 4) * 256 + lp * 4 + (i % 4));  // elem_index<E >= 4>
         }
-    if (int rc = build_banked(c, sets, 16, 16, &c->d_invb)) return rc;
+    // (the kernel's h-steps per table block: SA_F64_KH in binary64, SA_F32_KH at CB = 4)
+    const int kh = SA_SECB_COMPACT ? (sgn ? SA_F32_KH : SA_F64_KH) : c->nhi / 2;
+    if (int rc = build_banked(c, sets, 16, 16, &c->d_invb, kh)) return rc;
   }
   // the codeword-interleaved k_secb's copy of its bucket table with each
   // lane's E entries of a step contiguous (one 16-byte load per lane and
@@ -5167,7 +5207,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
   } else if (share) {  // sa_create_twin: the same tables, read-only, borrowed
     c->d_inv = share->d_inv; c->d_inv32 = share->d_inv32; c->d_invb = share->d_invb;
     c->d_fwdb = share->d_fwdb; c->d_fwd = share->d_fwd; c->d_fwd2 = share->d_fwd2; c->d_fwd3 = share->d_fwd3;
-    c->d_invl = share->d_invl;
+    c->d_invl = share->d_invl; c->d_hs = share->d_hs;
     c->invb_done = share->invb_done;
     c->borrowed = true;
   } else {
@@ -5531,6 +5571,7 @@ void sa_destroy(sa_ctx* c) {
     dev_free(c->d_invb);
     dev_free(c->d_fwdb);
     dev_free(c->d_invl);
+    dev_free(c->d_hs);
     dev_free(c->d_fwd);
     dev_free(c->d_fwd2);
     dev_free(c->d_fwd3);

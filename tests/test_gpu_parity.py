@@ -916,3 +916,30 @@ def test_decide_async_matches_decide(sp, B):
         op.decide_collect(B, 0)  # already collected
     with pytest.raises(AssertionError):
         op.decide_async(B, op.DECIDE_SLOTS)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_twin_operator_bit_identical(sp, prec):
+    """sa_create_twin (SparcOperator.twin, the joint pipeline's slices): a
+    second context over the source's device tables decodes a batch bit for bit
+    like the source (the batched kernel, with the bank-aware tables built
+    before the twin borrows them), and the source keeps decoding after the
+    twin is destroyed (the twin frees none of the borrowed tables)."""
+    import gc
+    L, M = 64, 256
+    n = int(L * np.log2(M))
+    B, T = 8, 6
+    Ab, _, ordering = orc.sparc_transforms(L, M, n)
+    Pl = 4.0 / L * np.ones(L)
+    ys = np.stack([orc.rep_inputs(L, M, n, Pl, 0.4, Ab, 700 + i)[1].reshape(-1) for i in range(B)])
+    op = sp.SparcOperator(L, M, n, ordering, precision=prec)
+    assert op.plan(B)["section_kernel"] == "k_secb"
+    ref, iref = op.amp_batch(ys, Pl, T, early_stop=False)
+    tw = op.twin()
+    assert tw.plan(B) == op.plan(B)
+    got, igot = tw.amp_batch(ys, Pl, T, early_stop=False)
+    assert np.array_equal(got, ref) and np.array_equal(igot, iref)
+    del tw
+    gc.collect()
+    again, _ = op.amp_batch(ys, Pl, T, early_stop=False)
+    assert np.array_equal(again, ref)

@@ -584,6 +584,42 @@ __device__ __forceinline__ void fwht_wave_sgn_pair(float (&x)[E], float (&y)[E],
   bfly_swap<32, float, E>(y);
 }
 
+// exp(x) for x <= 0 in binary64 from a 64-entry table of 2^(j/64) in LDS:
+// k = rint(x 64 / ln 2), r = x - k ln2/64 (Cody-Waite, |r| <= ln2/128),
+// e^x = 2^(k >> 6) 2^((k & 63)/64) e^r with e^r by a degree-5 polynomial
+// (truncation below 4e-17): within two ulps of the correctly rounded value;
+// 0 below -745.2 (where exp underflows to 0) and for -inf.
+__constant__ double c_exp2_64[64] = {  // 2^(j/64), correctly rounded (generated with decimal, 80 digits)
+    0x1.0000000000000p+0, 0x1.02c9a3e778061p+0, 0x1.059b0d3158574p+0, 0x1.0874518759bc8p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0e3ec32d3d1a2p+0, 0x1.11301d0125b51p+0, 0x1.1429aaea92de0p+0,
+    0x1.172b83c7d517bp+0, 0x1.1a35beb6fcb75p+0, 0x1.1d4873168b9aap+0, 0x1.2063b88628cd6p+0,
+    0x1.2387a6e756238p+0, 0x1.26b4565e27cddp+0, 0x1.29e9df51fdee1p+0, 0x1.2d285a6e4030bp+0,
+    0x1.306fe0a31b715p+0, 0x1.33c08b26416ffp+0, 0x1.371a7373aa9cbp+0, 0x1.3a7db34e59ff7p+0,
+    0x1.3dea64c123422p+0, 0x1.4160a21f72e2ap+0, 0x1.44e086061892dp+0, 0x1.486a2b5c13cd0p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4f9b2769d2ca7p+0, 0x1.5342b569d4f82p+0, 0x1.56f4736b527dap+0,
+    0x1.5ab07dd485429p+0, 0x1.5e76f15ad2148p+0, 0x1.6247eb03a5585p+0, 0x1.6623882552225p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6dfb23c651a2fp+0, 0x1.71f75e8ec5f74p+0, 0x1.75feb564267c9p+0,
+    0x1.7a11473eb0187p+0, 0x1.7e2f336cf4e62p+0, 0x1.82589994cce13p+0, 0x1.868d99b4492edp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8f1ae99157736p+0, 0x1.93737b0cdc5e5p+0, 0x1.97d829fde4e50p+0,
+    0x1.9c49182a3f090p+0, 0x1.a0c667b5de565p+0, 0x1.a5503b23e255dp+0, 0x1.a9e6b5579fdbfp+0,
+    0x1.ae89f995ad3adp+0, 0x1.b33a2b84f15fbp+0, 0x1.b7f76f2fb5e47p+0, 0x1.bcc1e904bc1d2p+0,
+    0x1.c199bdd85529cp+0, 0x1.c67f12e57d14bp+0, 0x1.cb720dcef9069p+0, 0x1.d072d4a07897cp+0,
+    0x1.d5818dcfba487p+0, 0x1.da9e603db3285p+0, 0x1.dfc97337b9b5fp+0, 0x1.e502ee78b3ff6p+0,
+    0x1.ea4afa2a490dap+0, 0x1.efa1bee615a27p+0, 0x1.f50765b6e4540p+0, 0x1.fa7c1819e90d8p+0};
+__device__ __forceinline__ double exp_neg_tab(double x, const double* tab) {
+  const double kd = __builtin_rint(x * 0x1.71547652b82fep+6);  // x 64 / ln 2
+  double r = fma(kd, -0x1.62e42fefa0000p-7, x);                  // ln2/64, high part (exact products)
+  r = fma(kd, -0x1.cf79abc9e3b3ap-46, r);  // ln2/64, low part
+  const int k = (int)kd;
+  double p = fma(r, 1.0 / 120, 1.0 / 24);
+  p = fma(r, p, 1.0 / 6);
+  p = fma(r, p, 0.5);
+  p = fma(r, p, 1.0);
+  p = fma(r, p, 1.0);
+  const double y = __builtin_amdgcn_ldexp(tab[k & 63] * p, k >> 6);
+  return x < -745.2 ? 0.0 : y;
+}
+
 template <typename real> __device__ __forceinline__ real dsqrt(real x);
 template <> __device__ __forceinline__ float dsqrt<float>(float x) { return sqrtf(x); }
 template <> __device__ __forceinline__ double dsqrt<double>(double x) { return sqrt(x); }
@@ -2100,6 +2136,10 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 #ifndef SA_SECB_COMPACT
 #define SA_SECB_COMPACT 1
 #endif
+//   SA_F64_EXPTAB  binary64 denoiser exp from a 64-entry LDS table (exp_neg_tab)
+#ifndef SA_F64_EXPTAB
+#define SA_F64_EXPTAB 1
+#endif
 #ifndef SA_ROWC_U12
 #define SA_ROWC_U12 1
 #endif
@@ -2195,6 +2235,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   const int zslots = (((n + kInvbZeroRows) * CB * (int)sizeof(real) + 15) / 16 * 16) / (int)sizeof(real);
   const int region = zslots > W * M * CB ? zslots : W * M * CB;
   real* bbw = zs + region;                   // [W][CB]
+  // binary64 (SA_F64_EXPTAB): the exp table, 64 doubles after bbw
+  constexpr bool XT = F64 && SA_F64_EXPTAB;
+  double* xtab = reinterpret_cast<double*>(bbw + W * CB);
+  if constexpr (XT) {
+    if (tid < 64) xtab[tid] = c_exp2_64[tid];  // read after the z barrier
+  }
 
   // codeword-interleaved z (a.zil: [NC][n][CB], 16-byte rows): this chunk's
   // rows straight into LDS by LDS-DMA (1 KB per wave instruction), issued
@@ -2461,7 +2507,10 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     real s = 0, s2 = 0;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      v[c][i] = dexp<real>(v[c][i] - mx[c]);  // :217; exp(-inf) = 0 on idle lanes
+      if constexpr (XT)
+        v[c][i] = (real)exp_neg_tab((double)(v[c][i] - mx[c]), xtab);  // :217
+      else
+        v[c][i] = dexp<real>(v[c][i] - mx[c]);  // :217; exp(-inf) = 0 on idle lanes
       s += v[c][i];
       s2 += v[c][i] * v[c][i];
     }
@@ -5127,7 +5176,7 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       for (int cb = (s == 4 ? 4 : 2); cb >= 1 && M <= 1024; cb >>= 1) {
         const size_t zb = (((size_t)(n + kInvbZeroRows) * cb * s) + 15) / 16 * 16;
         const size_t tb = (size_t)W * M * cb * s;
-        const size_t need = (zb > tb ? zb : tb) + (size_t)W * cb * s;
+        const size_t need = (zb > tb ? zb : tb) + (size_t)W * cb * s + (s == 8 && SA_F64_EXPTAB ? 64 * 8 : 0);
         if (need <= (cb == 1 || W > kWB ? 160 : 80) * 1024) return {cb, need};
       }
       return {0, 0};

@@ -498,7 +498,12 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-iters", type=int, default=0,
                     help="AMP iterations per CPU-baseline process (default: T, a whole decode)")
     ap.add_argument("--no-fp64", action="store_true", help="skip the binary64 leg of an fp32 run")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.plan and args.backend == "matrix":
+        # the device-generated Gaussian design (sa_create_matrix_random) takes
+        # no plan options: refuse rather than ignore them
+        ap.error("--plan applies to the hadamard / dense backends, not --backend matrix")
+    return args
 
 
 def main(argv=None, make_op=None):

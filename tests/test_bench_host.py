@@ -161,3 +161,13 @@ def test_load_trace_reads_the_exclusive_duration():
     tr = bench.load_trace("c2", "k_sec4")
     assert tr is not None and tr["duration_ns"] > 0 and tr["launches"] > 0
     assert tr["exclusive_ns"] is not None and tr["exclusive_ns"] > 0
+
+
+def test_plan_with_matrix_backend_is_refused():
+    """--plan with --backend matrix used to be silently ignored
+    (the device-generated design takes no plan); it is an argument error now."""
+    import bench
+    with pytest.raises(SystemExit):
+        bench.parse_args(["--backend", "matrix", "--plan", "ONE_PASS"])
+    assert bench.parse_args(["--backend", "matrix"]).plan == ""
+    assert bench.parse_args(["--plan", "ONE_PASS"]).plan == "ONE_PASS"

@@ -2140,6 +2140,9 @@ __device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ush
 #ifndef SA_F64_EXPTAB
 #define SA_F64_EXPTAB 1
 #endif
+#ifndef SA_GATHER_PRIO
+#define SA_GATHER_PRIO 3
+#endif
 #ifndef SA_ROWC_U12
 #define SA_ROWC_U12 1
 #endif
@@ -2395,6 +2398,9 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   STAMP(2);
 
   // ---- bucket gather of the CB codewords (one LDS access per row index) ----
+  // (SA_GATHER_PRIO: the gather at a raised wave priority, so every wave's
+  // latency-bound gather runs before the older waves' VALU-bound denoise)
+  if (SA_GATHER_PRIO) __builtin_amdgcn_s_setprio(SA_GATHER_PRIO);
   real v[CB][E];
 #pragma unroll
   for (int c = 0; c < CB; ++c)
@@ -2462,6 +2468,7 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   }
   if constexpr (LATE_F) load_f();
   if constexpr (LATE_B) load_section_nt<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lpos, M);
+  if (SA_GATHER_PRIO) __builtin_amdgcn_s_setprio(0);
   STAMP(3);
   // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
   // codewords with their section max / sums reduced together (wave_reduce_cb)

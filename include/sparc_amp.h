@@ -292,6 +292,10 @@ int sa_host_residual(sa_ctx* ctx, int B, int t, int flags, const double* ab);
  * 2 k_rowv 16-byte rows, 3 k_rowv 8-byte rows, 0 k_row, 4 k_row2 16-row
  * blocks, 5 k_rowc), number of CUs}. */
 int sa_plan(sa_ctx* ctx, int B, int64_t* out8);
+/* The batched section kernel's work order for B codewords (k_secb, B >= 4):
+ * out4 = {section groups, sections per workgroup, section groups per XCD per
+ * pass, passes per XCD}; SA_ERR_ARG when a decode of B does not run k_secb. */
+int sa_plan_batched(sa_ctx* ctx, int B, int64_t* out4);
 int sa_info(const sa_ctx* ctx, int64_t* out8); /* L, M, n, w, backend, precision, device, bytes */
 int sa_device_count(void);
 const char* sa_last_error(void);

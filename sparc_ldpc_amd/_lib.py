@@ -66,7 +66,7 @@ EXPORTS = (
     "sa_profile", "sa_profile_rep", "sa_profile_dispatch", "sa_profile_kinds", "sa_decide",
     "sa_decide_async", "sa_decide_collect", "sa_info", "sa_device_count", "sa_last_error", "sa_version",
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
-    "sa_threshold", "sa_cancel", "sa_plan", "sa_stage_onehot_scaled", "sa_cancel_scaled",
+    "sa_threshold", "sa_cancel", "sa_plan", "sa_plan_batched", "sa_stage_onehot_scaled", "sa_cancel_scaled",
     "sa_host_init", "sa_host_tau", "sa_host_eta", "sa_host_residual",
 )
 
@@ -107,6 +107,7 @@ _SIG = {
     "sa_threshold": (_I, [_P, _I, _I, _I, _P, _I, ct.c_double, ct.POINTER(ct.c_int32)]),
     "sa_cancel": (_I, [_P, _I, ct.POINTER(ct.c_int32), _P]),
     "sa_plan": (_I, [_P, _I, ct.POINTER(ct.c_int64)]),
+    "sa_plan_batched": (_I, [_P, _I, ct.POINTER(ct.c_int64)]),
     "sa_stage_onehot": (_I, [_P, _I, ct.POINTER(ct.c_int32)]),
     "sa_stage_onehot_scaled": (_I, [_P, _I, ct.POINTER(ct.c_int32), ct.c_double]),
     "sa_cancel_scaled": (_I, [_P, _I, ct.POINTER(ct.c_int32), ct.c_double, _P]),
@@ -126,13 +127,13 @@ _INC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 
 
 def source_hash() -> str:
-    """SHA-256 (first 16 hex digits) over the HIP sources and C headers the
-    libraries are built from (csrc/*.hip, csrc/Makefile, include/*.h, in name
-    order): the identity a committed profile records and bench.py compares
+    """SHA-256 (first 16 hex digits) over the HIP sources and headers the
+    libraries are built from (csrc/*.hip, csrc/*.h, csrc/Makefile, include/*.h,
+    in name order): the identity a committed profile records and bench.py compares
     against, so a roofline figure is only read from a profile of this build."""
     import hashlib
     h = hashlib.sha256()
-    files = sorted(f for f in os.listdir(_SRC_DIR) if f.endswith(".hip") or f == "Makefile")
+    files = sorted(f for f in os.listdir(_SRC_DIR) if f.endswith((".hip", ".h")) or f == "Makefile")
     paths = [os.path.join(_SRC_DIR, f) for f in files]
     if os.path.isdir(_INC_DIR):
         paths += [os.path.join(_INC_DIR, f) for f in sorted(os.listdir(_INC_DIR)) if f.endswith(".h")]

@@ -34,8 +34,6 @@ constexpr int kFKB = 128;                      // K bytes per LDS row per stage
 constexpr int kFStage = (kFTX + kFTY) * kFKB;  // 40960 B
 constexpr int kFLds = 2 * kFStage;             // double buffered: 80 KB
 constexpr int kFDma = (kFTX + kFTY) / 8;       // wave-level DMA instructions per stage (8 rows each)
-constexpr int kFMinB = 4;                      // batches at least this large take the GEMM path
-constexpr int kFMaxS = 16;                     // K splits of the A beta GEMM (its Ab partials)
 
 template <typename real>
 struct FArgs {

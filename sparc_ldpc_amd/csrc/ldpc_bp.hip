@@ -323,23 +323,8 @@ struct TailArgs {
   int* lastbad;          // [2][B]
   int Nv, Nc, Nmsg, B, n, S, it;
   int dyn;               // 1: n and the stop test from device memory
-  int prio;              // 1: the waves raise their issue priority (tail_prio)
   double corr;
 };
-
-// Issue priority of the tail's waves on their SIMDs.  Beside another stream's
-// full-chip kernel (the other slice of a pipelined joint batch: k_secb holds
-// every CU's LDS but leaves VGPRs for a few more waves per SIMD) the tail's
-// waves land on SIMDs shared with its waves, and at equal priority the
-// dependent Lxor chains get a fraction of the issue slots: an iteration ran
-// ~3x longer.  The highest wave priority lets them issue first (their chains
-// use a small share of the slots); results are unaffected.  Measured neutral
-// (2113-2119 vs 2114-2115 codewords/s): the tail's launches wait for whole
-// CUs, not for issue slots (k_secb<double> holds every CU's registers), so it
-// stays off by default (LDPC_BP_WAVE_PRIO=1 turns it on).
-__device__ __forceinline__ void tail_prio(const TailArgs& a) {
-  if (a.prio) __builtin_amdgcn_s_setprio(3);
-}
 
 // words still running in this tail launch; 0 when every word is done
 __device__ __forceinline__ int tail_words(const TailArgs& a) {
@@ -352,7 +337,6 @@ __device__ __forceinline__ int tail_words(const TailArgs& a) {
 // and message loaded at once, summed in port order with exact selects
 template <int DV>
 __global__ void __launch_bounds__(256) k_bp_tail_var(TailArgs a) {
-  tail_prio(a);
   const int n = tail_words(a);
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   for (int wi = blockIdx.y; wi < n; wi += gridDim.y) {
@@ -397,7 +381,6 @@ template <int ALGO, int DCMAX, int DCFIX>
 __global__ void __launch_bounds__(DCFIX > 0 ? kTailFixThreads : kTailThreads) k_bp_tail_chk(TailArgs a) {
   constexpr int ROW = DCMAX + 1;
   __shared__ double rows[DCFIX > 0 ? 1 : kTailThreads * ROW];
-  tail_prio(a);
   const int n = tail_words(a);
   const int cpw = (a.Nc + a.S - 1) / a.S;
   for (int item = blockIdx.x; item < n * a.S; item += gridDim.x) {
@@ -568,7 +551,6 @@ struct lb_ctx {
   int est_n = 0, est_B = 0, est_Bq = 0;  // the last landed count and its batch; the batch in flight
   int capTailB = 0;
   int tail_default = 0;       // tail_at chosen at lb_create (kTailAt or LDPC_BP_TAIL)
-  int wave_prio = 0;          // tail waves at the highest issue priority (LDPC_BP_WAVE_PRIO=1; measured neutral)
   int* d_vedge = nullptr;
   uint8_t* d_vdeg = nullptr;
   int* d_cstart = nullptr;
@@ -772,7 +754,6 @@ int launch(lb_ctx* c, int B, const double* d_ch, double* d_app, int* d_it, int a
   t.n = n;
   t.S = S;
   t.dyn = sized_on_host ? 0 : 1;
-  t.prio = c->wave_prio;
   t.corr = corr;
   double* slot[2] = {c->d_msg, c->d_msg + (size_t)B * c->Nmsg};
   const TailFn chk = pick_tail(algo, c->maxdc, split);
@@ -959,10 +940,6 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
     c->tail_at = (e && *e) ? std::max(0, atoi(e)) : kTailAt;
   }
   c->tail_default = c->tail_at;
-  {
-    const char* wp = getenv("LDPC_BP_WAVE_PRIO");
-    c->wave_prio = (wp && *wp && atoi(wp) == 1) ? 1 : 0;
-  }
   int rc = LB_OK;
   auto bail = [&](int r) { release(c); return r; };
   if (hipSetDevice(device) != hipSuccess) return bail(fail(LB_ERR_HIP, "hipSetDevice failed"));
@@ -974,15 +951,10 @@ int lb_create(lb_ctx** out, const long* vdeg, const long* cdeg, const long* intr
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0) c->ncu = ncu;
   }
-  // LDPC_BP_PRIORITY=1: the decoder's stream at the device's highest
-  // priority (measured slower beside a pipelined joint batch's AMP stream:
-  // 1945 vs 2100 codewords/s, so the default priority stays)
-  int prio_lo = 0, prio_hi = 0;
-  const char* pe = getenv("LDPC_BP_PRIORITY");
-  const bool high = pe && *pe && atoi(pe) == 1;
-  if (high && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
-  if ((high ? hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi)
-            : hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+  // (the stream at the device's highest priority, and the tail's waves at the
+  // highest issue priority, measured slower / neutral beside a pipelined joint
+  // batch's AMP stream, rounds 4-5: default priorities)
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(LB_ERR_HIP, "stream/event creation failed"));
   // uploads on the context's non-blocking stream, waited for (a pageable

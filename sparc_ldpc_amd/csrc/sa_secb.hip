@@ -1,0 +1,729 @@
+// sa_secb.hip — the batched section kernel k_secb (B codewords share the
+// operator) and its launcher.
+#include "sa_host.h"
+
+namespace sa {
+
+// ---------------------------------------------------------------------------
+// Batched section kernel (B codewords share the operator)
+// ---------------------------------------------------------------------------
+// One workgroup = 4 wavefronts x CB codewords, sweeping kSG = 16 consecutive
+// sections in 4 rounds of 4.  z of the CB codewords is staged interleaved
+// ([row][CB]) so one LDS gather fetches the same row of every codeword
+// (ds_read_b64 for CB = 2 fp32); the staged T_l = H_M beta_l are interleaved
+// the same way ([section][k][CB]); the Ab contributions of all 16 sections are
+// accumulated per row in LDS and written once (G = L / 16 partials).  The
+// bucket / Ab tables are read once per workgroup for CB codewords, and all
+// workgroups of a section group are placed on one XCD (blockIdx % 8 labels
+// the XCD) so the group's tables stay in that XCD's L2.
+
+template <typename real, int CB>
+struct cbvec;
+template <> struct cbvec<float, 1> { using t = float; };
+template <> struct cbvec<float, 2> { using t = float2; };
+template <> struct cbvec<float, 4> { using t = float4; };
+template <> struct cbvec<double, 1> { using t = double; };
+template <> struct cbvec<double, 2> { using t = double2; };
+
+template <typename real, int CB>
+__device__ __forceinline__ void vload(const real* p, real (&o)[CB]) {
+  using V = typename cbvec<real, CB>::t;
+  const V t = *reinterpret_cast<const V*>(p);
+  if constexpr (CB == 1) {
+    o[0] = t;
+  } else if constexpr (CB == 2) {
+    o[0] = t.x; o[1] = t.y;
+  } else {
+    o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = t.w;
+  }
+}
+template <typename real, int CB>
+__device__ __forceinline__ void vstore(real* p, const real (&o)[CB]) {
+  using V = typename cbvec<real, CB>::t;
+  V t;
+  if constexpr (CB == 1) {
+    t = o[0];
+  } else if constexpr (CB == 2) {
+    t.x = o[0]; t.y = o[1];
+  } else {
+    t.x = o[0]; t.y = o[1]; t.z = o[2]; t.w = o[3];
+  }
+  *reinterpret_cast<V*>(p) = t;
+}
+
+// LDS byte offset of the 16-bit row index in half `HALF` of w, scaled by
+// 2^SH (the [row][CB] element size): one SDWA VALU op (word select + shift).
+template <int SH, int HALF>
+__device__ __forceinline__ unsigned sdwa_shl16(unsigned w) {
+  unsigned r;
+  if constexpr (HALF == 0)
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+        : "=v"(r) : "v"(w), "i"(SH));
+  else
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+        : "=v"(r) : "v"(w), "i"(SH));
+  return r;
+}
+
+
+// One h-step of the bucket gather for E >= 4 (Q = 4): the wave's 4*NQ
+// bucket rows are turned into LDS addresses, all E gathers are issued, then
+// v[c][i] += sgn(h) * z[row][c] as fmas with a wave-uniform sign.
+template <typename real, int E, int CB>
+__device__ __forceinline__ void gather_step4(const unsigned char* zsb, const ushort4 (&t)[(E + 3) / 4],
+                                             real sg, real (&v)[CB][E]) {
+  constexpr int SH = ilog2c<CB * (int)sizeof(real)>();
+  unsigned ad[E];
+#pragma unroll
+  for (int j = 0; j < E / 4; ++j) {
+    const uint2 w = *reinterpret_cast<const uint2*>(&t[j]);
+    ad[4 * j + 0] = sdwa_shl16<SH, 0>(w.x);
+    ad[4 * j + 1] = sdwa_shl16<SH, 1>(w.x);
+    ad[4 * j + 2] = sdwa_shl16<SH, 0>(w.y);
+    ad[4 * j + 3] = sdwa_shl16<SH, 1>(w.y);
+  }
+  // zsb is the start of the dynamic LDS region, which is LDS address 0 in
+  // this kernel (it declares no static LDS: checked on the host at context
+  // creation), so the scaled row index is the LDS address itself.
+  (void)zsb;
+  using V = real __attribute__((ext_vector_type(CB)));
+  using lds_v = __attribute__((address_space(3))) const V;
+  real zz[E][CB];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const V x = *reinterpret_cast<lds_v*>((size_t)ad[i]);
+#pragma unroll
+    for (int c = 0; c < CB; ++c) zz[i][c] = x[c];
+  }
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) v[c][i] = fma(zz[i][c], sg, v[c][i]);
+}
+
+// Measured choices of k_secb (round 5, interleaved A/B, every choice bit-identical):
+//  * bucket h-steps with table loads in flight: 2 (binary32 at CB = 4 or E = 16,
+//    binary64: kSecbKH32 / kSecbKH64, sa_common.h); KH = 4 spilled
+//  * the first Ab-table rows and codeword 0's previous estimate loaded after
+//    the gather (their registers are free there): binary32 C3 +1.5 %; binary64
+//    with tau_{t-1} through the scalar cache and the gather sign a constant of
+//    each half of the bank-aware step order: C3 fp64 7.03 k -> 7.46 k cw/s
+//  * the gather at a raised wave priority (kGatherPrio), so every wave's
+//    latency-bound gather runs before the older waves' VALU-bound denoiser
+//  * binary32: the section transforms of codeword pairs interleaved
+//  * binary64: the denoiser's exp from a 64-entry LDS table (exp_neg_tab)
+constexpr int kGatherPrio = 3;
+template <typename real, int E, int CB, int W, bool ZIL = false>
+__global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NT = W * 64;
+  constexpr int NQ = (E + 3) / 4;
+  // binary64: fewer loads in flight so a wave fits 128 VGPRs (two workgroups per CU)
+  constexpr bool F64 = sizeof(real) == 8;
+  // bucket h-steps with table loads in flight together
+  constexpr int KH = F64 ? kSecbKH64 : ((E >= 16 || CB >= 4) ? kSecbKH32 : 4);
+  // binary64: the first Ab-table rows loaded after the gather instead of with
+  // the first loads (their registers are then free for the table stream)
+  constexpr bool LATE_F = true;
+  // binary64: the previous estimate of codeword 0 loaded after the gather too
+  constexpr bool LATE_B = !(CB <= 2 && !F64);
+  // rows per thread whose Ab-table loads are in flight together (one with 16
+  // sections at CB = 4: their 4 table words per row already fill the registers)
+  constexpr int KR = (CB >= 4 || F64) ? (W > 8 && (CB >= 4 || F64) ? 1 : 2) : 3;
+  constexpr bool PB = CB <= 2 && !F64;           // prefetch the previous beta with the first loads
+  constexpr int W4 = W / 4;             // 4-section table groups per workgroup
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int M = a.M, n = a.n;
+  const size_t LM = (size_t)a.L * M;
+  const int mlanes = M < 64 ? M : 64;
+  // SGN (binary32, E >= 2): both transforms run fwht_wave_sgn, which leaves
+  // slot k (lane L) with (-1)^<k,m> = sgl times the transform, m the two
+  // index bits on lane bits 0 / 1.  Cancelled exactly with no table change:
+  // the bucket gather and beta use quad-mirrored section positions (lane L
+  // holds index k ^ m: lane L ^ 3's) and the gathered input is multiplied by
+  // sgl.  With H(x(. ^ m))[k] = (-1)^<k,m> (Hx)[k] the first transform then
+  // yields Az at the mirrored positions with no sign (the denoiser and beta
+  // stay in that layout) and the second, fed mirrored beta, T = H beta in
+  // natural positions with no sign: the same values, bit for bit, as
+  // fwht_wave on the natural layout.
+  constexpr bool SGN = sizeof(real) == 4 && E >= 2;
+  const int lpos = SGN ? (lane ^ 3) : lane;  // section positions of this lane
+  const real sgl = (SGN && (__popc(lane & 3) & 1)) ? (real)-1 : (real)1;
+  const float s1 = (lane & 1) ? -1.f : 1.f, s2 = (lane & 2) ? -1.f : 1.f;
+  STAMP(0);
+
+  // XCD-grouped work mapping (speed only: any placement is correct)
+  int g, chunk;
+  {
+    const int bid = blockIdx.x, total = a.G * a.NC;
+    if ((a.G & 7) == 0 && (total & 7) == 0) {
+      const int x = bid & 7, j = bid >> 3;
+      // the XCD's G/8 section groups in passes of gpx groups, the groups of
+      // a pass fastest: the workgroups in flight on one XCD cover the pass's
+      // tables and a few codeword chunks' z, which stay in its L2 together
+      // (C4: 6 groups' tables, 4.7 MB, overflowed the 4 MB L2; two passes of 3)
+      const int gx = a.G >> 3;
+      int jj = j, g0 = 0, gp = a.gpx < gx ? a.gpx : gx;
+      while (jj >= gp * a.NC) {  // whole passes before this item (at most G / 8 steps)
+        jj -= gp * a.NC;
+        g0 += gp;
+        gp = gx - g0 < gp ? gx - g0 : gp;
+      }
+      g = (g0 + jj % gp) * 8 + x;
+      chunk = jj / gp;
+    } else {
+      g = bid / a.NC;
+      chunk = bid % a.NC;
+    }
+  }
+  int bc[CB];
+  bool valid[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const int b = chunk * CB + c;
+    valid[c] = b < a.B;
+    bc[c] = valid[c] ? b : a.B - 1;
+  }
+  const int l = g * W + wv;
+  const bool have = l < a.L;
+  const int lc = have ? l : a.L - 1;
+
+  // z ([n+1][CB], read by the bucket gather) and T ([W][M][CB], read by the
+  // Ab gather) are never live together: they share one LDS region.
+  real* zs = reinterpret_cast<real*>(smem);
+  real* ts = zs;
+  // z rows, then kInvbZeroRows zero rows (empty bucket slots; one per 16-B bank group)
+  const int zslots = (((n + kInvbZeroRows) * CB * (int)sizeof(real) + 15) / 16 * 16) / (int)sizeof(real);
+  const int region = zslots > W * M * CB ? zslots : W * M * CB;
+  real* bbw = zs + region;                   // [W][CB]
+  // binary64: the exp table, 64 doubles after bbw
+  constexpr bool XT = F64;
+  double* xtab = reinterpret_cast<double*>(bbw + W * CB);
+  if constexpr (XT) {
+    if (tid < 64) xtab[tid] = c_exp2_64[tid];  // read after the z barrier
+  }
+
+  // codeword-interleaved z (a.zil: [NC][n][CB], 16-byte rows): this chunk's
+  // rows straight into LDS by LDS-DMA (1 KB per wave instruction), issued
+  // before anything else; no register staging, no ds_write, no second pass
+  // (a template parameter: the two z paths in one kernel cost the binary64
+  // instantiations 32 bytes more scratch)
+  static_assert(!ZIL || CB * sizeof(real) == 16, "codeword-interleaved rows are 16 bytes");
+  constexpr bool zil = ZIL;
+  if (zil) {
+    const char* zsrc = reinterpret_cast<const char*>(a.z) + (size_t)chunk * n * CB * sizeof(real);
+    const int nbytes = n * CB * (int)sizeof(real);
+    for (int ch = wv; ch * 1024 < nbytes; ch += W) {
+      const int off = ch * 1024 + lane * 16;
+      if (off + 16 <= nbytes)  // rows are 16 bytes: whole rows only
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(zsrc + off),
+                                         (__attribute__((address_space(3))) void*)((char*)zs + ch * 1024), 16, 0, 0);
+    }
+  }
+  // ---- every load independent of z in flight together ---------------------
+  // the z^2 partials of the CB codewords first: tau waits for these alone
+  ZZParts<real, F64 ? 2 : 3> zzc[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) zzc[c].issue(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, lane);
+  // tau_{t-1} of the CB codewords (the exact-tau stop) right behind them: a
+  // load issued after the table loads would make the stop test wait for all
+  // of them (vmcnt retires in order), one more round trip per codeword
+  // (binary64 keeps the late load: at 128 VGPRs the early one costs spills)
+  real lastv[CB];
+  if constexpr (!F64) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+  } else {
+    // binary64: through the scalar cache, no VGPRs (tau_{t-1} was written by the previous launch)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_smem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+  }
+  // z rows of the CB codewords (first pass of the staging loop)
+  constexpr int KZ = 4;
+  real zr[KZ][CB];
+  // uniform codeword bases + 32-bit unsigned row offsets (SGPR-base loads)
+  const real* zc[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) zc[c] = a.z + (size_t)bc[c] * n;
+  if (!zil) {
+#pragma unroll
+    for (int u = 0; u < KZ; ++u) {
+      const int r = u * NT + tid;
+#pragma unroll
+      for (int c = 0; c < CB; ++c) zr[u][c] = ld_off(zc[c], (unsigned)(r < n ? r : 0) * (unsigned)sizeof(real));
+    }
+  }
+  // the bank-aware step order (build_invb: sign +1 steps first) or h order
+  const bool banked = a.invb != nullptr;
+  // binary32: a workgroup-uniform base + this wave's 32-bit offset (SGPR-base
+  // loads; binary64 keeps the per-wave pointer, its scratch grew otherwise)
+  const uint16_t* il = (banked ? a.invb : a.inv) + (size_t)lc * a.w;
+  auto load_tb = [&](int h0, ushort4 (&dst)[KH][NQ]) {
+    if constexpr (ZIL && E % 4 == 0) {
+      // lane-major table: this lane's NQ quads of step h in one run of E * 2 bytes
+      const uint16_t* base = a.invl + (size_t)lc * a.nhi * 64 * E + (size_t)lane * E;
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh) {
+        const int h = h0 + hh < a.nhi ? h0 + hh : a.nhi - 1;
+#pragma unroll
+        for (int j = 0; j < NQ; j += 2) {
+          if (j + 1 < NQ) {
+            const uint4 q = *reinterpret_cast<const uint4*>(base + (size_t)h * 64 * E + 4 * j);
+            dst[hh][j] = *reinterpret_cast<const ushort4*>(&q.x);
+            dst[hh][j + 1] = *reinterpret_cast<const ushort4*>(&q.z);
+          } else {
+            dst[hh][j] = *reinterpret_cast<const ushort4*>(base + (size_t)h * 64 * E + 4 * j);
+          }
+        }
+      }
+    } else if constexpr (F64)
+      load_buckets<E, KH>(il, h0, a.nhi, M, lpos, dst);
+    else
+      load_buckets_off<E, KH>((banked ? a.invb : a.inv) + (size_t)g * W * a.w, (unsigned)((lc - g * W) * a.w), h0,
+                              a.nhi, M, lpos, dst);
+  };
+  ushort4 tb[KH][NQ];
+  load_tb(0, tb);
+  // previous beta: all CB codewords up front when registers allow (CB <= 2),
+  // else codeword 0 now and codeword c+1 while c is denoised (PB false)
+  real bprev[PB ? CB : 2][E];
+  if constexpr (PB) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+      load_section_nt<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, bprev[c], lpos, M);
+  } else if constexpr (!LATE_B) {
+    load_section_nt<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lpos, M);
+  }
+  real cl[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) cl[c] = ld_vmem(a.c + (size_t)bc[c] * a.cst + lc);
+  // the Ab table rows: [W4][npad] of this group (rows past npad: whole waves,
+  // every lane reading row 0, a broadcast)
+  const int npad = (n + 63) & ~63;
+  const ushort4* fw = a.fwdb + (size_t)g * W4 * npad;
+  ushort4 f[KR][W4];
+  auto load_f = [&]() {
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      const int r = u * NT + tid;
+#pragma unroll
+      for (int q = 0; q < W4; ++q) f[u][q] = fw[(size_t)q * npad + (r < npad ? r : 0)];
+    }
+  };
+  if constexpr (!LATE_F) load_f();
+  // tau per codeword (sparc_ldpc.py:203-209)
+  bool live[CB];
+  bool any = false;
+  real tau2[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const real tau = zzc[c].tau(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
+    const bool stop = a.early_stop && (tau == lastv[c]);
+    if (valid[c] && g == 0 && tid == 0) {
+      a.tau[(size_t)bc[c] * a.T1 + a.t] = tau;
+      if (stop && a.iters[bc[c]] < 0) a.iters[bc[c]] = a.t;
+    }
+    live[c] = valid[c] && !stop;
+    any |= live[c];
+    tau2[c] = tau * tau;
+  }
+  if (!any) {  // uniform
+    if (zil) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write may outlive the workgroup
+    return;
+  }
+  STAMP(1);
+
+  // ---- z -> LDS interleaved [row][CB] ------------------------------------
+  if (zil) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed (the barrier: every wave's)
+  for (int r0 = 0; r0 < (zil ? 0 : n); r0 += KZ * NT) {
+#pragma unroll
+    for (int u = 0; u < KZ; ++u) {
+      const int r = r0 + u * NT + tid;
+      if (r < n) vstore<real, CB>(zs + (size_t)r * CB, zr[u]);
+    }
+    if (r0 + KZ * NT < n) {
+#pragma unroll
+      for (int u = 0; u < KZ; ++u) {
+        const int r = r0 + KZ * NT + u * NT + tid;
+#pragma unroll
+        for (int c = 0; c < CB; ++c) zr[u][c] = ld_off(zc[c], (unsigned)(r < n ? r : 0) * (unsigned)sizeof(real));
+      }
+    }
+  }
+  if (tid < kInvbZeroRows * CB) zs[(size_t)n * CB + tid] = 0;
+  __syncthreads();
+  STAMP(2);
+
+  // ---- bucket gather of the CB codewords (one LDS access per row index) ----
+  // (kGatherPrio: the gather at a raised wave priority, so every wave's
+  // latency-bound gather runs before the older waves' VALU-bound denoise)
+  __builtin_amdgcn_s_setprio(kGatherPrio);
+  real v[CB][E];
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[c][i] = 0;
+  {
+    constexpr int Q = E < 4 ? E : 4;
+    // one block of KH h-steps; sgf >= 0: every step of the block has that
+    // sign (the bank-aware order's halves), else sgn(h) per step
+    // hn: the next block's first step (< 0: none)
+    auto block = [&](int h0, int sgf, int hn) {
+      ushort4 tn[KH][NQ];
+      const bool more = hn >= 0;
+      if (more) load_tb(hn, tn);
+#pragma unroll
+      for (int hh = 0; hh < KH; ++hh) {
+        if (h0 + hh < a.nhi) {
+          // sgn(h): the high index bits of w-M+c are all ones; in the bank-aware
+          // order the slots of sign -1 are the second half of the steps
+          const bool neg = sgf >= 0 ? sgf == 1 : (banked ? (h0 + hh >= (a.nhi >> 1)) : (__popc(h0 + hh) & 1));
+          const real sg = neg ? -sgl : sgl;
+          if constexpr (E >= 4) {
+            gather_step4<real, E, CB>(reinterpret_cast<const unsigned char*>(zs), tb[hh], sg, v);
+          } else {
+            const ushort4 r4 = tb[hh][0];
+            const unsigned short rr4[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+              real zz[CB];
+              vload<real, CB>(zs + (size_t)rr4[q] * CB, zz);
+#pragma unroll
+              for (int c = 0; c < CB; ++c) v[c][q] = fma(zz[c], sg, v[c][q]);
+            }
+          }
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int hh = 0; hh < KH; ++hh)
+#pragma unroll
+          for (int j = 0; j < NQ; ++j) tb[hh][j] = tn[hh][j];
+      }
+    };
+    const int half = a.nhi >> 1;
+    // (the 16-byte-row configurations up to M = 512: elsewhere the duplicated
+    // loop body spilled)
+    constexpr bool GS = CB * sizeof(real) == 16 && E <= 8;
+    if (GS && banked && half > 0 && half % KH == 0) {
+      // the bank-aware order: the +1 steps, then the -1 steps; the sign is a
+      // constant of each loop (the same fmas with the same signs).  Each half
+      // holds its occupied slots in its first s0 / s1 steps (build_invb: the
+      // section's largest column count, a multiple of KH): the rest, empty
+      // for every column, is skipped
+      int s0 = half, s1 = half;
+      if (a.hs) {
+        const unsigned v = a.hs[__builtin_amdgcn_readfirstlane(lc)];
+        s0 = (int)(v & 0xffffu);
+        s1 = (int)(v >> 16);
+      }
+      for (int h0 = 0; h0 < s0; h0 += KH) block(h0, 0, h0 + KH < s0 ? h0 + KH : (s1 > 0 ? half : -1));
+      for (int h0 = half; h0 < half + s1; h0 += KH) block(h0, 1, h0 + KH < half + s1 ? h0 + KH : -1);
+    } else {
+      for (int h0 = 0; h0 < a.nhi; h0 += KH) block(h0, -1, h0 + KH < a.nhi ? h0 + KH : -1);
+    }
+  }
+  if constexpr (LATE_F) load_f();
+  if constexpr (LATE_B) load_section_nt<real, E>(a.beta + (size_t)bc[0] * LM + (size_t)lc * M, bprev[0], lpos, M);
+  __builtin_amdgcn_s_setprio(0);
+  STAMP(3);
+  // denoiser eta (sparc_ldpc.py:213-219, as denoise_section) of the CB
+  // codewords with their section max / sums reduced together (wave_reduce_cb)
+  const int ml = E >= 2 ? 64 : mlanes;  // E >= 2: M = 64 E fills every lane
+  auto fwht_sec = [&](real (&x)[E]) {
+    if constexpr (SGN) fwht_wave_sgn<E>(x, s1, s2);
+    else fwht_wave<real, E>(x, lane, ml);
+  };
+  // binary32 codeword pairs: the two transforms of a pair interleaved
+  constexpr bool FP = SGN && CB % 2 == 0 && E >= 2;
+  auto fwht_all = [&]() {
+    if constexpr (FP) {
+#pragma unroll
+      for (int c = 0; c < CB; c += 2) fwht_wave_sgn_pair<E>(v[c], v[c + 1], s1, s2);
+    }
+  };
+  fwht_all();
+  const real inv_sn = (real)1 / a.sqrt_n;
+  real bbl[CB], mx[CB], S[CB], S2[CB];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    if constexpr (!PB) {
+      if (c + 1 < CB)
+        load_section_nt<real, E>(a.beta + (size_t)bc[c + 1] * LM + (size_t)lc * M, bprev[(c + 1) & 1], lpos, M);
+    }
+    if constexpr (!FP) fwht_sec(v[c]);
+    const real k = cl[c] / tau2[c];
+    real m = neg_inf<real>();
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      // :213, :215.  The exponent argument below, u - max, is contracted to
+      // fma(s, k, -max) (one rounding where the reference rounds u first:
+      // <= 1 ulp of u, inside the parity bounds; 4 % faster at c3)
+      const real u = fma(v[c][i], inv_sn, bprev[PB ? c : (c & 1)][i]) * k;
+      v[c][i] = (E >= 2 || elem_index<E>(lane, i) < M) ? u : neg_inf<real>();
+      m = max_raw(m, v[c][i]);  // one v_max (operands finite or -inf)
+    }
+    mx[c] = m;
+  }
+  wave_reduce_cb<true, CB>(mx);  // :216 (per section)
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    real s = 0, s2 = 0;
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if constexpr (XT)
+        v[c][i] = (real)exp_neg_tab((double)(v[c][i] - mx[c]), xtab);  // :217
+      else
+        v[c][i] = dexp<real>(v[c][i] - mx[c]);  // :217; exp(-inf) = 0 on idle lanes
+      s += v[c][i];
+      s2 += v[c][i] * v[c][i];
+    }
+    S[c] = s;
+    S2[c] = s2;
+  }
+  wave_reduce_cb<false, CB>(S);   // :218
+  wave_reduce_cb<false, CB>(S2);  // sum(beta^2)
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    const real scale = cl[c] / S[c];  // :219
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[c][i] *= scale;
+    if (have && live[c]) store_section_nt<real, E>(a.beta + (size_t)bc[c] * LM + (size_t)lc * M, v[c], lpos, M);
+    if (have) {
+      bbl[c] = S2[c] * scale * scale;
+      if constexpr (!FP) fwht_sec(v[c]);  // T_l = H_M beta_l (natural positions)
+    } else {
+      bbl[c] = 0;
+#pragma unroll
+      for (int i = 0; i < E; ++i) v[c][i] = 0;
+    }
+  }
+  if (have) fwht_all();  // (FP) the T transforms of the codeword pairs
+  STAMP(4);
+  __syncthreads();  // every wave is done with z before T overwrites it
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = elem_index<E>(lane, i);
+    if (e < M) {
+      real o[CB];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) o[c] = v[c][i];
+      // staged at t_pos(e): consecutive lanes write consecutive rows (in
+      // natural order a lane's Q elements are adjacent, and the store of one
+      // register by 64 lanes has a Q-row stride: a Q-way bank conflict)
+      constexpr int Q = E < 4 ? E : 4;
+      vstore<real, CB>(ts + ((size_t)wv * M + (i / Q) * 64 * Q + (i % Q) * 64 + lane) * CB, o);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < CB; ++c) bbw[wv * CB + c] = bbl[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    if (tid == c && live[c]) {
+      real t = 0;
+      for (int w2 = 0; w2 < W; ++w2) t += bbw[w2 * CB + c];
+      a.bbp[(size_t)bc[c] * a.G + g] = t;
+    }
+  }
+  STAMP(5);
+  // ---- Ab partial of the workgroup's W sections for every row ---------------
+  // (each row's W table entries in its own bank-aware order, build_fwdb: the
+  // entry holds the staged T element s * M + k itself)
+  constexpr int SHB = ilog2c<CB * (int)sizeof(real)>();      // T element k -> byte k << SHB
+  for (int r0 = 0; r0 < n; r0 += KR * NT) {
+    ushort4 fn[KR][W4];
+    const bool more = r0 + KR * NT < n;
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < KR; ++u) {
+        const int r = r0 + KR * NT + u * NT + tid;
+#pragma unroll
+        for (int q = 0; q < W4; ++q) fn[u][q] = fw[(size_t)q * npad + (r < npad ? r : 0)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KR; ++u) {
+      const int r = r0 + u * NT + tid;
+      real acc[CB];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) acc[c] = 0;
+#pragma unroll
+      for (int q = 0; q < W4; ++q) {
+        const uint2 w = *reinterpret_cast<const uint2*>(&f[u][q]);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          // entry = k | sign << 15: T element k of section q*4+s4, sign -> +-1.0
+          const unsigned wd = s4 < 2 ? w.x : w.y;
+          const bool up = s4 & 1;
+          real t[CB];
+          real sg;
+          if constexpr (sizeof(real) == 4) {
+            // binary32: k and the LDS byte address in two ops, the sign
+            // bit ORed into 1.0f (one op for the upper half-word)
+            const unsigned k = up ? __builtin_amdgcn_ubfe(wd, 16, 15) : (wd & 0x7fffu);
+            const unsigned sb = (up ? wd : wd << 16) & 0x80000000u;
+            sg = __uint_as_float(sb | 0x3f800000u);
+            using V = real __attribute__((ext_vector_type(CB)));
+            using lds_v = __attribute__((address_space(3))) const V;
+            // ts is LDS address 0 (the dynamic region, no static LDS)
+            const V x = *reinterpret_cast<lds_v*>((size_t)(k << SHB));
+#pragma unroll
+            for (int c = 0; c < CB; ++c) t[c] = x[c];
+          } else {
+            const unsigned hw = up ? wd >> 16 : wd;
+            const unsigned k = __builtin_amdgcn_ubfe(hw, 0, 15);
+            sg = (hw & 0x8000u) ? (real)-1 : (real)1;
+            vload<real, CB>(ts + (size_t)k * CB, t);
+          }
+#pragma unroll
+          for (int c = 0; c < CB; ++c) acc[c] = fma(t[c], sg, acc[c]);
+        }
+      }
+      if (r < n) {
+        if (zil) {  // one 16-byte vector of the CB codewords ([NC][G][n][CB])
+          using V = real __attribute__((ext_vector_type(CB)));
+          V pv;
+#pragma unroll
+          for (int c = 0; c < CB; ++c) pv[c] = acc[c];
+          __builtin_nontemporal_store(pv, reinterpret_cast<V*>(a.abp) + ((size_t)chunk * a.G + g) * n + r);
+        } else {
+#pragma unroll
+          for (int c = 0; c < CB; ++c)
+            if (live[c]) st_part(&a.abp[((size_t)bc[c] * a.G + g) * n + r], acc[c]);
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < KR; ++u)
+#pragma unroll
+        for (int q = 0; q < W4; ++q) f[u][q] = fn[u][q];
+    }
+  }
+#ifdef SA_STAMPS
+  STAMP(6);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(7);
+#endif
+}
+
+// ---- launchers ------------------------------------------------------------
+
+// Batched section kernel: grid = Gb groups x ceil(B / CB) chunks (1-D, XCD-grouped).
+template <typename real, int E, int CB>
+void launch_secb_e(sa_ctx* c, int B, SecArgs<real> a) {
+  a.G = c->Gb;
+  a.B = B;
+  a.NC = (B + CB - 1) / CB;
+  a.zil = zil_for(c, B) ? 1 : 0;
+  a.gpx = c->gpx;
+  if (c->prof) c->prof->begin(c->stream, K_SEC);
+  const dim3 grid(c->Gb * a.NC);
+  bool done = false;
+  if constexpr (CB * sizeof(real) == 16) {
+    if (a.zil) {
+      if (c->WB == kWB16)
+        plaunch(c, k_secb<real, E, CB, kWB16, true>, grid, kWB16 * 64, c->secb_lds, a);
+      else
+        plaunch(c, k_secb<real, E, CB, kWB, true>, grid, kWB * 64, c->secb_lds, a);
+      done = true;
+    }
+  }
+  if (!done) {
+    if (c->WB == kWB16)
+      plaunch(c, k_secb<real, E, CB, kWB16>, grid, kWB16 * 64, c->secb_lds, a);
+    else
+      plaunch(c, k_secb<real, E, CB, kWB>, grid, kWB * 64, c->secb_lds, a);
+  }
+  if (c->prof) c->prof->end(c->stream);
+}
+
+template <typename real, int CB>
+int launch_secb_cb(sa_ctx* c, int B, const SecArgs<real>& a) {
+  switch (c->E) {
+    case 1: launch_secb_e<real, 1, CB>(c, B, a); break;
+    case 2: launch_secb_e<real, 2, CB>(c, B, a); break;
+    case 4: launch_secb_e<real, 4, CB>(c, B, a); break;
+    case 8: launch_secb_e<real, 8, CB>(c, B, a); break;
+    case 16: launch_secb_e<real, 16, CB>(c, B, a); break;
+    default: return fail(SA_ERR_UNSUPPORTED, "batched kernel: M > 1024");
+  }
+  return SA_OK;
+}
+
+template <typename real>
+int launch_secb(sa_ctx* c, int B, int t, int es) {
+  SecArgs<real> a = sec_args<real>(c, SEC_AMP, t, es);
+  int rc;
+  if constexpr (sizeof(real) == 4) {
+    if (c->CB == 4) {
+      rc = launch_secb_cb<real, 4>(c, B, a);
+      if (rc) return rc;
+      HIP_TRY(hipGetLastError());
+      return SA_OK;
+    }
+  }
+  if (c->CB == 2) rc = launch_secb_cb<real, 2>(c, B, a);
+  else rc = launch_secb_cb<real, 1>(c, B, a);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  return SA_OK;
+}
+
+template int launch_secb<float>(sa_ctx*, int, int, int);
+template int launch_secb<double>(sa_ctx*, int, int, int);
+
+// Every k_secb instantiation may use the full 160 KB LDS.
+template <typename real>
+static hipError_t secb_lds_attrs_t() {
+  const int mx = 160 * 1024;
+  hipError_t e = hipSuccess;
+#define SA_A(F) if (e == hipSuccess) e = hipFuncSetAttribute((const void*)F, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+#define SA_AW(CB, W, Z) SA_A((k_secb<real, 1, CB, W, Z>)) SA_A((k_secb<real, 2, CB, W, Z>)) \
+  SA_A((k_secb<real, 4, CB, W, Z>)) SA_A((k_secb<real, 8, CB, W, Z>)) SA_A((k_secb<real, 16, CB, W, Z>))
+  SA_AW(1, kWB, false) SA_AW(2, kWB, false) SA_AW(1, kWB16, false) SA_AW(2, kWB16, false)
+  if constexpr (sizeof(real) == 8) {  // codeword-interleaved (16-byte rows: CB = 2)
+    SA_AW(2, kWB, true) SA_AW(2, kWB16, true)
+  }
+  if constexpr (sizeof(real) == 4) {
+    SA_AW(4, kWB, false) SA_AW(4, kWB16, false) SA_AW(4, kWB, true) SA_AW(4, kWB16, true)
+  }
+#undef SA_AW
+#undef SA_A
+  return e;
+}
+
+hipError_t secb_lds_attrs() {
+  hipError_t e = secb_lds_attrs_t<float>();
+  return e == hipSuccess ? secb_lds_attrs_t<double>() : e;
+}
+
+// gather_step4 addresses LDS absolutely: the batched kernel must have no
+// static LDS in front of its dynamic region.
+template <typename real>
+static bool secb_no_static_lds_t() {
+  hipFuncAttributes at;
+  const void* fs[] = {(const void*)k_secb<real, 4, 1, kWB>, (const void*)k_secb<real, 8, 1, kWB>,
+                      (const void*)k_secb<real, 16, 1, kWB>, (const void*)k_secb<real, 8, 2, kWB>,
+                      (const void*)k_secb<real, 16, 2, kWB>, (const void*)k_secb<real, 8, 2, kWB16>,
+                      (const void*)k_secb<real, 16, 2, kWB16>, (const void*)k_secb<real, 8, 1, kWB16>};
+  for (const void* f : fs)
+    if (hipFuncGetAttributes(&at, f) != hipSuccess || at.sharedSizeBytes != 0) return false;
+  return true;
+}
+
+bool secb_no_static_lds() { return secb_no_static_lds_t<float>() && secb_no_static_lds_t<double>(); }
+
+#ifdef SA_STAMPS
+hipError_t stamps_add_secb(unsigned long long* out) {
+  unsigned long long s[16 * 16];
+  hipError_t e = hipMemcpyFromSymbol(s, HIP_SYMBOL(g_stamps), sizeof(s));
+  for (int i = 0; i < 16 * 16; ++i) out[i] += s[i];
+  return e;
+}
+#endif
+
+}  // namespace sa

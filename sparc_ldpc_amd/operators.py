@@ -317,6 +317,14 @@ class SparcOperator:
                     codewords_per_wg=int(o[3]), zz_partials=int(o[4]), w=int(o[5]),
                     row_kernel={1: "k_row2", 2: "k_rowv16B", 3: "k_rowv8B", 4: "k_row2_16", 5: "k_rowc"}.get(int(o[6]), "k_row"), cus=int(o[7]))
 
+    def plan_batched(self, B):
+        """The batched section kernel's work order for B codewords
+        (sa_plan_batched): section groups, sections per workgroup, groups per
+        XCD per pass, passes per XCD."""
+        o = np.zeros(4, dtype=np.int64)
+        check(self._lib.sa_plan_batched(self._ctx, int(B), o.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int64))))
+        return dict(groups=int(o[0]), sections_per_wg=int(o[1]), groups_per_pass=int(o[2]), passes=int(o[3]))
+
     def info(self):
         o = np.zeros(8, dtype=np.int64)
         check(self._lib.sa_info(self._ctx, o.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int64))))

@@ -714,6 +714,69 @@ def test_c2_batch256_golden(sp, prec):
         assert argmax_agree(b2[s], ref, L, M), s
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_c4_batch256_golden(sp, prec):
+    """BASELINE configs[3] at the benched launch shape: 256 codewords of C4
+    (L=768 M=512 R=5/6, n=8294) in one decode, which runs k_secb + k_rowc
+    with 48 section groups in two passes per XCD (the c4 bench line).  The
+    reference's two C4 codewords (c4.npz) sit in slots 0 and 1 and codeword 0
+    again in slot 255 (the last codeword chunk): t = 1, t = 8 (binary64) and
+    the estimate at the exact-tau stop against the reference's (binary32: the
+    fixture's first NS sections at 1e-5 and the norm; binary64: c4_f64.npz at
+    1e-11) and every section's statistics (sections.npz); four seeded slots
+    spread over the chunks against the oracle at t = 2
+    (sparc_ldpc.py:189-222, amp_test.py:14-50)."""
+    g = golden("c4.npz")
+    L, M, n, T, NS = (int(g[k]) for k in ("L", "M", "n", "T", "NS"))
+    B = 256
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=prec)
+    plan = op.plan(B)
+    assert plan["section_kernel"] == "k_secb" and plan["row_kernel"] == "k_rowc", plan
+    wo = op.plan_batched(B)
+    assert wo["groups"] == 48 and wo["passes"] == 2, wo  # 6 groups per XCD in 2 passes of 3
+    Pl = float(g["P"]) / L * np.ones(L)
+    c = np.sqrt(n * Pl[0])
+    oAb, oAz, _ = orc.sparc_transforms(L, M, n)
+    gold = {0: 0, 1: 1, 255: 0}  # slot -> c4.npz codeword
+    seeded = (2, 77, 130, 254)   # chunks 0, 19, 32, 63
+    Y = np.empty((B, n))
+    for s in range(B):
+        if s in gold:
+            Y[s] = g[f"y_{gold[s]}"].reshape(-1)
+            continue
+        rs = np.random.RandomState(7000 + s)
+        b0 = np.zeros(L * M)
+        b0[np.arange(L) * M + rs.randint(0, M, L)] = c
+        Y[s] = rs.randn(n) * 0.7
+        Y[s] += (oAb(b0).reshape(-1) if s in seeded else op.Ab_batch(b0[None, :])[0])
+    g64 = golden("c4_f64.npz") if prec == "fp64" else None
+    b1, _ = op.amp_batch(Y, Pl, 1)
+    bf, it = op.amp_batch(Y, Pl, T)
+    b8 = op.amp_batch(Y, Pl, 8, early_stop=False)[0] if g64 is not None else None
+    for s, k in gold.items():
+        check_sections(b1[s], f"c4_{k}_t1", L, M, c, prec)
+        check_sections(bf[s], f"c4_{k}_final", L, M, c, prec)
+        assert np.array_equal(orc.section_argmax(bf[s], L, M), g[f"argmax_final_{k}"]), s
+        if g64 is not None:
+            check_f64(b1[s], g64, "beta_t1", NS, M, k)
+            check_f64(b8[s], g64, "beta_t8", NS, M, k)
+            check_sections(b8[s], f"c4_{k}_t8", L, M, c, prec)
+            check_f64(bf[s], g64, "beta_final", NS, M, k)
+        else:
+            assert rel(b1[s, :NS * M], g[f"beta_t1_{k}"]) <= TOL[prec], s
+            assert abs(np.linalg.norm(b1[s]) / float(g[f"beta_t1_norm_{k}"]) - 1) <= TOL[prec], s
+            assert rel(bf[s, :NS * M], g[f"beta_final_{k}"]) <= TOL[prec], s
+            assert abs(np.linalg.norm(bf[s]) / float(g[f"beta_final_norm_{k}"]) - 1) <= TOL[prec], s
+    # the same codeword in the first and the last chunk: the same decode bit for bit
+    assert np.array_equal(bf[0], bf[255]) and it[0] == it[255]
+    assert np.all((it >= 0) & (it <= T))
+    b2, _ = op.amp_batch(Y, Pl, 2, early_stop=False)
+    for s in seeded:
+        ref = orc.amp(Y[s], 0, Pl, L, M, 2, oAb, oAz)
+        assert rel(b2[s], ref) <= TOL[prec], s
+        assert argmax_agree(b2[s], ref, L, M), s
+
+
 def test_c4_fp64_stop_index(sp):
     """The exact-tau stop (sparc_ldpc.py:204, amp_test.py:14-50) in binary64
     at C4: the estimate after the reference's own stop index t_ref (t_ref

@@ -103,9 +103,11 @@ class JointDecoder:
     """AMP operator + LDPC code + the shortened operator of the unprotected
     sections, for B-codeword batches of the joint schemes."""
 
-    def __init__(self, L, M, n, code, T, backend=None, precision=None, device=None, seed=0, twin_of=None):
+    def __init__(self, L, M, n, code, T, backend=None, precision=None, device=None, seed=0, twin_of=None,
+                 ordering=None):
         """twin_of: another JointDecoder whose operator tables this one shares
-        (SparcOperator.twin: own stream and workspace, one copy of the tables)."""
+        (SparcOperator.twin: own stream and workspace, one copy of the tables).
+        ordering: the design's (L, n) ordering (default: make_ordering(..., seed))."""
         self.L, self.M, self.n, self.T = int(L), int(M), int(n), int(T)
         self.logm = int(round(math.log2(M)))
         self.code = code
@@ -118,8 +120,11 @@ class JointDecoder:
             self.op = twin_of.op.twin()
             self.sub = twin_of.sub.twin() if twin_of.sub is not None else None
         else:
-            self.op = SparcOperator(L, M, n, make_ordering(L, M, n, seed), backend, precision, device)
+            if ordering is None:
+                ordering = twin_of.op.ordering if twin_of is not None else make_ordering(L, M, n, seed)
+            self.op = SparcOperator(L, M, n, ordering, backend, precision, device)
             self.sub = self.op.subset(np.arange(self.l0)) if self.l0 > 0 else None
+        self._pipeline = None  # joint_pipeline's cached JointPipeline over this decoder
         self.total_bits = self.L * self.logm
         self.R = (self.L * self.logm - (code.N - code.K)) / n  # sparc_ldpc.py:541
         self._masked = None  # full-size operator for the per-codeword masked decodes (threshold mode)
@@ -304,8 +309,10 @@ class JointPipeline:
         op, code = jd.op, jd.code
         for _ in range(int(parts) - 1):
             c2 = _ldpc.code(code.standard, code.rate, code.z, code.ptype, device=code._device)
+            # every slice decodes against jd's design (its ordering, whatever
+            # seed built it): the twin's shared tables or its own copy of them
             self.parts.append(JointDecoder(jd.L, jd.M, jd.n, c2, jd.T, op.backend, op.precision, op.device,
-                                           twin_of=jd if TWIN_SLICES else None))
+                                           twin_of=jd if TWIN_SLICES else None, ordering=op.ordering))
         self._pool = ThreadPoolExecutor(max_workers=len(self.parts), thread_name_prefix="joint")
         self._slices = None
 
@@ -362,7 +369,6 @@ class JointPipeline:
 
 
 _JD_CACHE: "OrderedDict[tuple, JointDecoder]" = OrderedDict()
-_JP_CACHE: "dict[int, JointPipeline]" = {}
 
 # batches of at least this many codewords are decoded as two concurrent halves
 PIPELINE_MIN_BATCH = 64
@@ -371,12 +377,23 @@ TWIN_SLICES = True
 
 
 def joint_pipeline(jd: JointDecoder, parts=2) -> JointPipeline:
-    """The cached JointPipeline over jd (the extra slices' tables built once)."""
-    jp = _JP_CACHE.get(id(jd))
-    if jp is None or jp.jd is not jd or len(jp.parts) != parts:
+    """The JointPipeline over jd, cached on jd itself (the extra slices' tables
+    and contexts built once, released with jd)."""
+    jp = jd._pipeline
+    if jp is None or len(jp.parts) != parts:
+        if jp is not None:
+            jp.close()
         jp = JointPipeline(jd, parts)
-        _JP_CACHE[id(jd)] = jp
+        jd._pipeline = jp
     return jp
+
+
+def _evict(jd: JointDecoder):
+    """A decoder leaving _JD_CACHE: its pipeline's thread pool and slices go too."""
+    if jd._pipeline is not None:
+        jd._pipeline.close()
+        jd._pipeline.parts = [jd]
+        jd._pipeline = None
 
 
 def joint_decoder(L, M, n, ldpcparams: LDPCParams, T, backend=None, precision=None, device=None):
@@ -397,7 +414,7 @@ def joint_decoder(L, M, n, ldpcparams: LDPCParams, T, backend=None, precision=No
         jd = JointDecoder(L, M, n, code, T, backend, precision, device)
         _JD_CACHE[key] = jd
         while len(_JD_CACHE) > 4:
-            _JD_CACHE.popitem(last=False)
+            _evict(_JD_CACHE.popitem(last=False)[1])
     else:
         _JD_CACHE.move_to_end(key)
     return jd
@@ -449,14 +466,16 @@ def mc_joint(jd: JointDecoder, Pl, sigma, seeds, mode, soft_iter=2, batch=256, t
     """Seeded batched reps: rep s draws from RandomState(s) in the reference's
     order.  Returns the per-rep error-count dict of JointDecoder.run, in seed
     order.  pipeline (default: batches of PIPELINE_MIN_BATCH or more in the
-    soft / hard / originalHard modes): decode each batch as two concurrent
-    halves (JointPipeline), with the same per-rep results."""
+    soft / hard / originalHard modes on the Hadamard backend, whose slices
+    share one copy of the tables): decode each batch as two concurrent halves
+    (JointPipeline), with the same per-rep results."""
     seeds = list(seeds)
     parts = []
     for s0 in range(0, len(seeds), batch):
         chunk = seeds[s0:s0 + batch]
         idx, noise = jd.draw([np.random.RandomState(s) for s in chunk], len(chunk), sigma)
-        pipe = pipeline if pipeline is not None else (len(chunk) >= PIPELINE_MIN_BATCH and mode != "threshold")
+        pipe = pipeline if pipeline is not None else (len(chunk) >= PIPELINE_MIN_BATCH and mode != "threshold"
+                                                      and jd.op.backend == "hadamard")
         runner = joint_pipeline(jd) if pipe else jd
         parts.append(runner.run(idx, noise, Pl, mode, soft_iter, threshold, unit_cancel))
     return {k: np.concatenate([p[k] for p in parts], axis=0) for k in parts[0]}

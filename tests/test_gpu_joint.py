@@ -177,3 +177,31 @@ def test_pipeline_equals_one_decoder():
         b = mc_joint(jd, Pl, spp.sigma, range(300, 371), mode, batch=71, pipeline=True)
         for k in a:
             assert np.array_equal(a[k], b[k]), (mode, k)
+
+
+def test_pipeline_slices_share_a_seeded_design():
+    """A JointDecoder on the design of ordering seed 3, pipelined with and
+    without twin slices: every slice decodes against the decoder's own design
+    (untwinned slices re-derived the seed-0 ordering), so the
+    per-rep results equal one decoder's over the batch."""
+    import sparc_ldpc_amd as sp
+    from sparc_ldpc_amd import joint
+    lp = sp.LDPCParams("802.16", "5/6", 8)
+    code = sp.code(lp.standard, lp.r_ldpc, lp.z)
+    jd = joint.JointDecoder(64, 16, 256, code, 30, precision="fp64", seed=3)
+    assert not np.array_equal(jd.op.ordering, sp.make_ordering(64, 16, 256, 0))
+    Pl = 4.0 / 64 * np.ones(64)
+    a = joint.mc_joint(jd, Pl, 0.95, range(400, 471), "soft", batch=71, pipeline=False)
+    twin = joint.TWIN_SLICES
+    try:
+        for tw in (True, False):
+            joint.TWIN_SLICES = tw
+            jd._pipeline = None
+            b = joint.mc_joint(jd, Pl, 0.95, range(400, 471), "soft", batch=71, pipeline=True)
+            for p in jd._pipeline.parts:
+                assert np.array_equal(p.op.ordering, jd.op.ordering)
+            for k in a:
+                assert np.array_equal(a[k], b[k]), (tw, k)
+            jd._pipeline.close()
+    finally:
+        joint.TWIN_SLICES = twin

@@ -53,18 +53,16 @@ def synth_y(op, Pl, sigma, seeds, with_idx=False):
     """Synthetic reps: RandomState(seed) -> L indices in [0, M),
     then N(0, σ²) noise; x = A β₀ on the device.  with_idx: also the (B, L)
     transmitted section indices."""
+    from sparc_ldpc_amd.harness import draw_reps
     L, M, n = op.L, op.M, op.n
     c = np.sqrt(n * Pl)
     B = len(seeds)
+    # RandomState(seed).randint(0, M, L) then .randn(n) * sigma, drawn natively
+    # (bit for bit NumPy's legacy generator, tests/test_host.py)
+    sent, noise = draw_reps(seeds, L, M, n, sigma)
     beta0 = np.zeros((B, L * M))
-    noise = np.empty((B, n))
-    sent = np.empty((B, L), dtype=np.int32)
-    for i, s in enumerate(seeds):
-        rs = np.random.RandomState(s)
-        idx = rs.randint(0, M, L)
-        sent[i] = idx
-        beta0[i, np.arange(L) * M + idx] = c
-        noise[i] = rs.randn(n) * sigma
+    for i in range(B):
+        beta0[i, np.arange(L) * M + sent[i]] = c
     y = op.Ab_batch(beta0) + noise
     return (y, sent) if with_idx else y
 
@@ -315,7 +313,7 @@ def load_pmc(workload, kernel):
         return None
 
 
-def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
+def measure_roofline(op, workload, L, M, n, B, T, precision, ms_per_step):
     """Roofline of the dominant kernel of one decode of B codewords.
 
     `achieved` = algorithmic bytes (ops) per launch / the kernel's launch
@@ -374,7 +372,7 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
     disp_ms = kinds_disp[dom][0]
     ev_ms = kinds_rep[dom][0]
     # the trace of the same command, if it was taken of these sources
-    tag = PROFILE_TAGS.get((args.workload, B, op.backend, precision))
+    tag = PROFILE_TAGS.get((workload, B, op.backend, precision))
     tr = load_trace(tag, trace_name) if tag else None
     matched = tr is not None and tr["sources"] == src
     if matched:
@@ -420,7 +418,7 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
         if matched:
             t["live_dispatch_over_trace"] = round(disp_ms / (tr["duration_ns"] * 1e-6), 4)
         roof["trace"] = t
-    pmc = load_pmc(f"{args.workload}_{op.backend}_{precision}_B{B}", trace_name)
+    pmc = load_pmc(f"{workload}_{op.backend}_{precision}_B{B}", trace_name)
     if pmc is not None:
         if pmc.get("sources") == src:
             roof["traffic"] = pmc.get("hbm_bytes_per_launch")
@@ -429,7 +427,7 @@ def measure_roofline(op, args, L, M, n, B, T, precision, ms_per_step):
             roof["traffic_stale"] = {"hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch"),
                                      "sources": pmc.get("sources"), "note": "PMC pass of other sources: not used"}
     if kname == "k_secb" and precision == "fp32":
-        vb = valu_bound(args.workload, kname, dom_ms, plan["cus"])
+        vb = valu_bound(workload, kname, dom_ms, plan["cus"])
         if vb is not None:
             roof["secondary_bound"] = dict(bound="latency", **vb)
     return roof
@@ -481,6 +479,99 @@ def timed_steps(op, B, T, steps, warmup, sent=None, decide=True):
             "section_errors": errs, "decided_steps": decided, "last_decisions": last}
 
 
+# The batched configurations timed beside the headline in the default line
+# (VERDICT r05 item 2): BASELINE configs[2] in binary32 and binary64, configs[3]
+# at its benched batch, and configs[3]'s 10 k-rep Monte-Carlo sweep as one
+# refilled stream (sa_mc_run).
+LEGS = (("c3", "c3", "fp32"), ("c3_fp64", "c3", "fp64"), ("c4", "c4", "fp32"))
+MC_SIGMAS = tuple(float(v) for v in np.linspace(0.8, 0.4, 10))  # soft_hard_plot's sigma points (sparc_ldpc.py:1318)
+MC_REPS_PER_POINT = 1000
+
+
+def batched_leg(sp, workload, precision, args, device, rank, world, make_op=None):
+    """One batched configuration with the headline's protocol (timed_steps:
+    decode + decision per step, max over ranks) and its own roofline."""
+    w = WORKLOADS[workload]
+    L, M, P, T, B, sigma = w["L"], w["M"], w["P"], w["T"], w["B"], w["sigma"]
+    n = n_of(w)
+    Pl = P / L * np.ones(L)
+    op = (make_op(L, M, n, "hadamard", precision, device, None) if make_op is not None else
+          sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision=precision, device=device))
+    y, sent = synth_y(op, Pl, sigma, [1000 + rank * B + i for i in range(B)], with_idx=True)
+    op.reserve(B, T)
+    op.stage(y, Pl)
+    ts = timed_steps(op, B, T, args.leg_steps, args.leg_warmup, sent)
+    ms = round(ts["elapsed"] / args.leg_steps * 1e3, 4)
+    plan = op.plan(B)
+    leg = {"workload": w["desc"], "value": round(B * args.leg_steps * world / ts["elapsed"], 3),
+           "unit": "codewords/s", "ms_per_step": ms, "steps": args.leg_steps, "warmup": args.leg_warmup,
+           "dtype": "f32" if precision == "fp32" else "f64", "codewords_per_step_per_gpu": B,
+           "section_kernel": plan["section_kernel"], "row_kernel": plan["row_kernel"],
+           "section_errors_rank0": ts["section_errors"], "decided_steps_rank0": ts["decided_steps"],
+           "roofline": measure_roofline(op, workload, L, M, n, B, T, precision, ms)}
+    del op
+    return leg
+
+
+def mc_stream_leg(sp, args, device, rank, world, make_op=None):
+    """configs[3]'s Monte-Carlo sweep (L=768 M=512 R=5/6 P=1.8, T=64, the exact-
+    tau stop on): MC_REPS_PER_POINT reps at each of the 10 sigma points, rep j
+    of point i seeded i * 100000 + j, sharded over the ranks; drawn natively
+    on the host cores, then decoded on the device as ONE stream through 256
+    refilled slots (sa_mc_run).  value = all ranks' reps / the slowest rank's
+    device time of the stream (encode of every rep, decode, decisions, bit
+    errors); the host draws and the staging are reported beside it."""
+    from sparc_ldpc_amd import dist
+    from sparc_ldpc_amd.harness import draw_reps
+    w = WORKLOADS["c4"]
+    L, M, P, T = w["L"], w["M"], w["P"], w["T"]
+    n = n_of(w)
+    Pl = P / L * np.ones(L)
+    op = (make_op(L, M, n, "hadamard", "fp32", device, None) if make_op is not None else
+          sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp32", device=device))
+    if not op.mc_supported(256):
+        return {"error": "the operator does not support the refilled stream"}
+    seeds = [[j for j in range(i * 100000, i * 100000 + MC_REPS_PER_POINT) if j % world == rank]
+             for i in range(len(MC_SIGMAS))]
+    cnt = [len(s) for s in seeds]
+    off = np.concatenate([[0], np.cumsum(cnt)]).astype(int)
+    idx = np.empty((off[-1], L), dtype=np.int32)
+    noise = np.empty((off[-1], n))
+    t0 = time.perf_counter()
+    for i, sg in enumerate(MC_SIGMAS):
+        draw_reps(seeds[i], L, M, n, sg, idx=idx[off[i]:off[i + 1]], noise=noise[off[i]:off[i + 1]])
+    t1 = time.perf_counter()
+    op.reserve(256, T)
+    op.stage_power(256, Pl)
+    op.mc_stage(idx, noise)
+    t2 = time.perf_counter()
+    op.mc_run(256, T, decisions=False)  # warm: tables, graphs
+    dist.barrier()
+    t3 = time.perf_counter()
+    _, its, errs, dev_ms = op.mc_run(256, T, decisions=False)
+    t4 = time.perf_counter()
+    dev_max = float(dist.allreduce_max(np.array([dev_ms]))[0])
+    tot = dist.allreduce_sum(np.array([off[-1], int(errs.sum()), int(its.sum()),
+                                       int(np.minimum(its + 1, T).sum())], dtype=np.int64))
+    per_point = dist.allreduce_sum(np.array([[int(errs[off[i]:off[i + 1]].sum()) for i in range(len(MC_SIGMAS))],
+                                             cnt], dtype=np.int64))
+    del op
+    return {
+        "workload": f"BASELINE configs[3]: L={L} M={M} R=5/6 P={P}, T={T}, exact-tau stop on, "
+                    f"{MC_REPS_PER_POINT} reps x {len(MC_SIGMAS)} sigma points (linspace(0.8, 0.4, 10)), "
+                    f"one refilled stream of 256 slots per GPU",
+        "value": round(float(tot[0]) / (dev_max * 1e-3), 1), "unit": "Monte-Carlo reps/s",
+        "reps": int(tot[0]), "stream_device_ms_max_over_ranks": round(dev_max, 3),
+        "stream_wall_ms_rank0": round((t4 - t3) * 1e3, 3),
+        "codeword_iterations": int(tot[2]), "slot_iterations": int(tot[3]),
+        "codeword_iterations_per_s": round(float(tot[2]) / (dev_max * 1e-3), 1),
+        "host_draw_ms_rank0": round((t1 - t0) * 1e3, 2), "stage_ms_rank0": round((t2 - t1) * 1e3, 2),
+        "ber_per_point": [round(float(e) / (c * L * np.log2(M)), 8) for e, c in zip(per_point[0], per_point[1])],
+        "note": "codeword_iterations: the sum of the stop indices (T when a rep ran out); slot_iterations: "
+                "the section / row steps the slots ran (min(stop index + 1, T) per rep)",
+    }
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -498,6 +589,11 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-iters", type=int, default=0,
                     help="AMP iterations per CPU-baseline process (default: T, a whole decode)")
     ap.add_argument("--no-fp64", action="store_true", help="skip the binary64 leg of an fp32 run")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the batched legs (configs[2] fp32 / fp64, configs[3], the configs[3] Monte-Carlo "
+                         "stream) of the default configs[1] line")
+    ap.add_argument("--leg-steps", type=int, default=10)
+    ap.add_argument("--leg-warmup", type=int, default=2)
     args = ap.parse_args(argv)
     if args.plan and args.backend == "matrix":
         # the device-generated Gaussian design (sa_create_matrix_random) takes
@@ -559,7 +655,7 @@ def main(argv=None, make_op=None):
     ms_per_step = round(elapsed / args.steps * 1e3, 4)
     # the decodes alone (no decision), same protocol: the round-4 definition of a step
     ts0 = timed_steps(op, B, T, args.steps, min(args.warmup, 1), decide=False)
-    roofline = measure_roofline(op, args, L, M, n, B, T, args.precision, ms_per_step)
+    roofline = measure_roofline(op, args.workload, L, M, n, B, T, args.precision, ms_per_step)
     result = {
         "metric": f"decoded codewords/sec (T AMP iters) at L={L},M={M}; achieved HBM GB/s vs roofline",
         "value": round(B * args.steps * world / elapsed, 3),
@@ -611,8 +707,17 @@ def main(argv=None, make_op=None):
         result["fp64_leg"] = {"value": round(B * args.steps * world / e64, 3), "unit": "codewords/s",
                               "ms_per_step": ms64, "dtype": "f64", "section_errors_rank0": t64["section_errors"],
                               "section_kernel": op64.plan(B)["section_kernel"],
-                              "roofline": measure_roofline(op64, args, L, M, n, B, T, "fp64", ms64)}
+                              "roofline": measure_roofline(op64, args.workload, L, M, n, B, T, "fp64", ms64)}
         del op64
+    if args.workload == "c2" and args.backend == "hadamard" and args.precision == "fp32" and not args.no_legs \
+            and not args.batch:
+        # the batched configurations, every rank, each with its own roofline
+        legs = {}
+        for tag, wl, prec in LEGS:
+            legs[tag] = batched_leg(sp, wl, prec, args, device, rank, world, make_op)
+        result["batched_legs"] = legs
+        if make_op is None:
+            result["mc_stream"] = mc_stream_leg(sp, args, device, rank, world)
     if rank == 0 and not args.no_dense:
         # after the timed region, on rank 0's GPU: the N-rank line carries the
         # dense GEMV probe as well

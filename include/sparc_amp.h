@@ -283,6 +283,39 @@ int sa_host_tau(sa_ctx* ctx, int B, int t, int flags, int* stopped);
 int sa_host_eta(sa_ctx* ctx, int B, int t, int flags, const double* az);
 int sa_host_residual(sa_ctx* ctx, int B, int t, int flags, const double* ab);
 
+/* Monte-Carlo rep stream (BASELINE configs[3]: amp_test.py:183-246, the BER
+ * sweeps of sparc_ldpc.py:1217-1245 / 1318-1323).
+ *
+ * sa_draw_reps: on the host cores, rep i drawn as NumPy's
+ * RandomState(seeds[i]).randint(0, M, L) (idx_out [count][L]) followed by
+ * .randn(n) * sigma (noise_out [count][n]), bit for bit NumPy's legacy
+ * generator (MT19937, masked bounded integers, polar Gaussian); threads <= 0:
+ * every hardware thread.
+ *
+ * sa_mc_stage copies `nreps` reps (section indices [nreps][L], noise
+ * [nreps][n], fp64) to the device.  sa_mc_run decodes them through B slots
+ * (4 <= B <= 1024) of the batched decode with per-slot refill: each slot runs
+ * its own iteration index, and when its exact-tau stop fires or T iterations
+ * are done its section decisions go to dec_out [nreps][L] and its stop index
+ * (T when the loop ran out) to iters_out [nreps], and the next rep is encoded
+ * into the slot (y = A beta(idx) + noise) on the device; errs_out [nreps]
+ * receives each rep's bit errors (the popcounts of decision ^ index summed
+ * over its sections, sparc_ldpc.py:462); any output may be NULL.  Every rep's
+ * decisions and stop index equal those of sa_encode + sa_run(early stop) +
+ * sa_decide on any batch holding it.  Needs one staged power allocation
+ * (sa_stage Pl) and the batched codeword-interleaved Hadamard decode
+ * (sa_plan: k_secb + k_rowc), else SA_ERR_UNSUPPORTED; ms_out: the device
+ * time of the whole stream (events), or NULL. */
+int sa_draw_reps(const uint32_t* seeds, int count, int L, int M, int n, double sigma, int32_t* idx_out,
+                 double* noise_out, int threads);
+int sa_mc_stage(sa_ctx* ctx, int nreps, const int32_t* idx, const double* noise);
+int sa_mc_run(sa_ctx* ctx, int B, int T, int flags, int32_t* dec_out, int32_t* iters_out, int32_t* errs_out,
+              double* ms_out);
+/* The design's row sub-sampling table (sparc_ldpc.py:107-117): NumPy's
+ * RandomState(seed) shuffling arange(1, w) once per section, cumulatively,
+ * the first n of each kept, w = 2^ceil(log2(max(M+1, n+1))); out [L][n]. */
+int sa_make_ordering(int L, int M, int n, uint32_t seed, uint32_t* out);
+
 /* Introspection. */
 /* The kernels a decode of B codewords runs: out8 = {section kernel (0 k_sec,
  * 1 k_sec2, 2 k_secb, 3 dense fp32 GEMVs, 4 k_sec4, 5 k_sec43, 6 dense int8

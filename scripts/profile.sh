@@ -23,7 +23,7 @@ run() {  # name, rocprof args...
 BENCH_ARGS=("$@")
 SCRIPT=${SCRIPT:-bench.py}
 EXTRA=(--no-cpu)
-[ "$SCRIPT" = bench.py ] && EXTRA+=(--no-dense)
+[ "$SCRIPT" = bench.py ] && EXTRA+=(--no-dense --no-legs)
 run trace --kernel-trace --stats && \
 run fetch --kernel-trace --pmc FETCH_SIZE && \
 run write --kernel-trace --pmc WRITE_SIZE

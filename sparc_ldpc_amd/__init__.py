@@ -12,7 +12,7 @@ from .operators import (SparcOperator, AbOp, AzOp, make_ordering, sub_fht, block
                         sparc_transforms, sparc_transforms_shorter, default_device)
 from .amp import amp, amp_test, amp_batch, operator_of
 from .harness import (SPARCParams, LDPCParams, pa_parameterised, bits2indices, ber_of,
-                      amp_ldpc_sim, mc_decode, ebno_to_sigma, ber_point, waterfall_plain,
+                      amp_ldpc_sim, mc_decode, mc_decode_batched, mc_stream, draw_reps, ebno_to_sigma, ber_point, waterfall_plain,
                       amp_test_reps, amp_init_test)
 from . import ldpc
 from .ldpc import code, LdpcBpError

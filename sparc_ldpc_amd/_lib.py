@@ -68,6 +68,7 @@ EXPORTS = (
     "sa_encode", "sa_stage_onehot", "sa_llr", "sa_soft_beta0", "sa_hard_cancel",
     "sa_threshold", "sa_cancel", "sa_plan", "sa_plan_batched", "sa_stage_onehot_scaled", "sa_cancel_scaled",
     "sa_host_init", "sa_host_tau", "sa_host_eta", "sa_host_residual",
+    "sa_draw_reps", "sa_mc_stage", "sa_mc_run", "sa_make_ordering",
 )
 
 _P = ct.c_void_p
@@ -118,6 +119,10 @@ _SIG = {
     "sa_host_tau": (_I, [_P, _I, _I, _I, ct.POINTER(ct.c_int)]),
     "sa_host_eta": (_I, [_P, _I, _I, _I, _D]),
     "sa_host_residual": (_I, [_P, _I, _I, _I, _D]),
+    "sa_draw_reps": (_I, [ct.POINTER(ct.c_uint32), _I, _I, _I, _I, ct.c_double, ct.POINTER(ct.c_int32), _D, _I]),
+    "sa_mc_stage": (_I, [_P, _I, ct.POINTER(ct.c_int32), _D]),
+    "sa_mc_run": (_I, [_P, _I, _I, _I, ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32), _D]),
+    "sa_make_ordering": (_I, [_I, _I, _I, ct.c_uint32, ct.POINTER(ct.c_uint32)]),
 }
 
 _lib = None

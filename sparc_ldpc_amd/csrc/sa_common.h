@@ -906,6 +906,9 @@ struct SecArgs {
   // groups whose tables one XCD's L2 holds at a time); >= G / 8: one pass
   int gpx;
   real sqrt_n;
+  // Monte-Carlo stream (sa_mc_run): per-codeword iteration index t_b (slot_t),
+  // -1 for an empty slot; null: every codeword is at iteration t
+  const int* tb;
 };
 
 template <typename real>
@@ -927,6 +930,7 @@ struct RowArgs {
   int Pbst;
   int pt;  // Ab partial layout (SecArgs::pt); k_row2 only
   int Bc;  // k_rowc: codewords of the decode (the last chunk may be partial)
+  const int* tb;  // k_rowc: per-codeword iteration index (SecArgs::tb), or null
 };
 
 // One workgroup = 4 wavefronts = 4 consecutive sections of one codeword
@@ -1169,6 +1173,29 @@ constexpr int kSecbKH32 = 2, kSecbKH64 = 2;
 
 template <int N>
 constexpr int ilog2c() { return N <= 1 ? 0 : 1 + ilog2c<N / 2>(); }
+
+// argmax of one section (one wave, lane's elements elem_index<E>), first index
+// on ties as np.argmax (sparc_ldpc.py:452-455); uniform over the wave
+template <typename real, int E>
+__device__ __forceinline__ int section_argmax(const real* bl, int lane, int M) {
+  real best = neg_inf<real>();
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = elem_index<E>(lane, i);
+    if (e < M) {
+      const real x = bl[e];
+      if (x > best || (x == best && e < bi)) { best = x; bi = e; }
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const real ob = __shfl_xor(best, m);
+    const int oi = __shfl_xor(bi, m);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  return bi == 0x7fffffff ? 0 : bi;
+}
 
 constexpr int kRow2Rows = 32;  // k_row2: one 128-B line of a partial per row block
 

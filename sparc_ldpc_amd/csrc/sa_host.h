@@ -138,6 +138,22 @@ struct sa_ctx {
   size_t dec_cap = 0;
   hipEvent_t dec_ev[SA_DECIDE_SLOTS] = {};
   int dec_B[SA_DECIDE_SLOTS] = {};
+  // Monte-Carlo stream (sa_mc_stage / sa_mc_run, sa_mc.hip): the staged reps'
+  // section indices [mc_cap][L] and noise [mc_cap][n], their decisions and stop
+  // indices, the slot state of the refilled batch, and its captured graphs
+  int mc_cap = 0, mc_nreps = 0;
+  int32_t *d_mc_idx = nullptr, *d_mc_dec = nullptr, *d_mc_its = nullptr;
+  double* d_mc_noise = nullptr;
+  void *d_mc_y = nullptr, *d_mc_zzp = nullptr;  // the staged reps encoded: y [mc_cap][n], z^2 partials [mc_cap][NZ2]
+  int* d_slots = nullptr;   // [4][slot_cap]: rep, t, done rep, fresh; then ctl {next, live, nreps}
+  int slot_cap = 0;
+  int* h_mc_live = nullptr;  // pinned ring of the live-slot counts the host polls
+  hipEvent_t mc_ev[4] = {};
+  const int* mc_tb = nullptr;  // the slots' t_b while an MC sequence is launched (SecArgs::tb)
+  std::map<std::tuple<int, int, int, int>, hipGraphExec_t> mc_graphs;
+  // host copies of the bucket table inv [L][w] and the Ab table fwd [G][n][4]
+  // (build_tables), kept until the batched tables are built from them (ensure_invb)
+  std::vector<uint16_t> h_inv, h_fwd;
 };
 
 namespace sa {
@@ -249,6 +265,7 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   a.cst = c->pb_on ? c->L : 0;
   if (c->pb_on) a.c = (const real*)c->d_cb;
   a.sqrt_n = (real)std::sqrt((double)c->n);
+  a.tb = c->mc_tb;
   return a;
 }
 
@@ -267,7 +284,26 @@ RowArgs<real> row_args(sa_ctx* c, int mode, int t, int early_stop, int G, int Gb
   a.Pbst = c->pb_on ? 1 : 0;
   a.pt = 0;
   a.Bc = 0;
+  a.tb = c->mc_tb;
   return a;
+}
+
+// f(i) for i in [0, count) over the host's cores (at most 16 threads), in
+// contiguous blocks of `grain` (callers write disjoint outputs per block)
+template <typename F>
+void parallel_for(int count, int grain, F f) {
+  const int blocks = (count + grain - 1) / grain;
+  unsigned nth = std::thread::hardware_concurrency();
+  nth = nth == 0 ? 1 : (nth > 16 ? 16 : nth);
+  if ((int)nth > blocks) nth = blocks > 0 ? blocks : 1;
+  auto run = [&](int t) {
+    for (int b = t; b < blocks; b += (int)nth)
+      for (int i = b * grain; i < count && i < (b + 1) * grain; ++i) f(i);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < (int)nth; ++t) th.emplace_back(run, t);
+  run(0);
+  for (auto& x : th) x.join();
 }
 
 // ---- defined in sparc_amp.hip ------------------------------------------------
@@ -281,6 +317,7 @@ int ensure_stage(sa_ctx* c, size_t count);
 int upload(sa_ctx* c, void* dst, const double* src, size_t count);
 int download(sa_ctx* c, double* dst, const void* src, size_t count);
 int set_power(sa_ctx* c, const double* Pl);
+int ensure_invb(sa_ctx* c);
 int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int backend, int prec, int device,
                 int plan, const sa_ctx* share = nullptr);
 extern __global__ void k_fill32(uint32_t* p, uint32_t v, size_t nw);
@@ -321,6 +358,10 @@ int i8_set_bfix(sa_ctx* c);
 int build_dense(sa_ctx* c);
 int matrix_init(sa_ctx* c);  // a caller's matrix: padded layout, zeroed d_A
 hipError_t dense_lds_attrs();
+
+// ---- sa_mc.hip: the Monte-Carlo rep stream ------------------------------------
+void mc_release(sa_ctx* c);  // its buffers and graphs (sa_destroy)
+hipError_t mc_lds_attrs();
 
 #ifdef SA_STAMPS
 hipError_t stamps_add_sec(unsigned long long* out);   // adds the unit's s_memtime stamps into out

@@ -195,14 +195,22 @@ __global__ void __launch_bounds__(256) k_rowc(RowArgs<real> a, int pil) {
     ro[k] = in[k] ? rr[k] : 0;
   }
   const int B = a.Bc;
-  int bc[CB];
+  int bc[CB], tcur[CB];
   bool valid[CB];
+  bool anyv = false;
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     const int b = chunk * CB + c;
     valid[c] = b < B;
     bc[c] = valid[c] ? b : B - 1;
+    tcur[c] = a.t;
+    if (a.tb) {  // Monte-Carlo stream: the slot's own iteration, -1 for an empty slot
+      tcur[c] = ld_smem(a.tb + bc[c]);
+      valid[c] = valid[c] && tcur[c] >= 0;
+    }
+    anyv |= valid[c];
   }
+  if (!anyv) return;  // uniform: a chunk of empty slots (Monte-Carlo stream tail)
   // wave 0's operands that do not depend on the partials, loaded with them
   real tau[CB], last[CB], yv[RPL][CB], bbv[CB][2];
   V zo[RPL] = {};
@@ -212,8 +220,8 @@ __global__ void __launch_bounds__(256) k_rowc(RowArgs<real> a, int pil) {
       tau[c] = 1;
       last[c] = 0;
       if (a.mode == ROW_AMP) {
-        tau[c] = ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t);
-        last[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+        tau[c] = ld_vmem(a.tau + (size_t)bc[c] * a.T1 + tcur[c]);
+        last[c] = tcur[c] > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + tcur[c] - 1) : (real)0;
         const real* bp = a.bbp + (size_t)bc[c] * a.Gb;
         bbv[c][0] = lane < a.Gb ? bp[lane] : (real)0;
         bbv[c][1] = lane + 64 < a.Gb ? bp[lane + 64] : (real)0;
@@ -413,24 +421,8 @@ __global__ void __launch_bounds__(256) k_decide(const real* beta, int32_t* idx, 
   const int lane = threadIdx.x & 63;
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6), b = blockIdx.y;
   if (l >= L) return;
-  const real* bl = beta + ((size_t)b * L + l) * M;
-  real best = neg_inf<real>();
-  int bi = 0x7fffffff;
-#pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const int e = elem_index<E>(lane, i);
-    if (e < M) {
-      const real x = bl[e];
-      if (x > best || (x == best && e < bi)) { best = x; bi = e; }
-    }
-  }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    const real ob = __shfl_xor(best, m);
-    const int oi = __shfl_xor(bi, m);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-  }
-  if (lane == 0) idx[(size_t)b * L + l] = bi == 0x7fffffff ? 0 : bi;
+  const int bi = section_argmax<real, E>(beta + ((size_t)b * L + l) * M, lane, M);
+  if (lane == 0) idx[(size_t)b * L + l] = bi;
 }
 
 // ---- launchers ------------------------------------------------------------

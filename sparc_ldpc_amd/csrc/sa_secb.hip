@@ -176,13 +176,18 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
       chunk = bid % a.NC;
     }
   }
-  int bc[CB];
+  int bc[CB], tcur[CB];
   bool valid[CB];
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     const int b = chunk * CB + c;
     valid[c] = b < a.B;
     bc[c] = valid[c] ? b : a.B - 1;
+    tcur[c] = a.t;
+    if (a.tb) {  // Monte-Carlo stream: the slot's own iteration, -1 for an empty slot
+      tcur[c] = ld_smem(a.tb + bc[c]);
+      valid[c] = valid[c] && tcur[c] >= 0;
+    }
   }
   const int l = g * W + wv;
   const bool have = l < a.L;
@@ -232,11 +237,11 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
   real lastv[CB];
   if constexpr (!F64) {
 #pragma unroll
-    for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+    for (int c = 0; c < CB; ++c) lastv[c] = tcur[c] > 0 ? ld_vmem(a.tau + (size_t)bc[c] * a.T1 + tcur[c] - 1) : (real)0;
   } else {
     // binary64: through the scalar cache, no VGPRs (tau_{t-1} was written by the previous launch)
 #pragma unroll
-    for (int c = 0; c < CB; ++c) lastv[c] = a.t > 0 ? ld_smem(a.tau + (size_t)bc[c] * a.T1 + a.t - 1) : (real)0;
+    for (int c = 0; c < CB; ++c) lastv[c] = tcur[c] > 0 ? ld_smem(a.tau + (size_t)bc[c] * a.T1 + tcur[c] - 1) : (real)0;
   }
   // z rows of the CB codewords (first pass of the staging loop)
   constexpr int KZ = 4;
@@ -320,8 +325,8 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
     const real tau = zzc[c].tau(a.zzp + (size_t)bc[c] * a.NZ, a.NZ, n);
     const bool stop = a.early_stop && (tau == lastv[c]);
     if (valid[c] && g == 0 && tid == 0) {
-      a.tau[(size_t)bc[c] * a.T1 + a.t] = tau;
-      if (stop && a.iters[bc[c]] < 0) a.iters[bc[c]] = a.t;
+      a.tau[(size_t)bc[c] * a.T1 + tcur[c]] = tau;
+      if (stop && a.iters[bc[c]] < 0) a.iters[bc[c]] = tcur[c];
     }
     live[c] = valid[c] && !stop;
     any |= live[c];

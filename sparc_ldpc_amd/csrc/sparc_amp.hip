@@ -86,6 +86,8 @@ void dev_free(void* p) {
 void drop_graphs(sa_ctx* c) {
   for (auto& kv : c->graphs) (void)hipGraphExecDestroy(kv.second);
   c->graphs.clear();
+  for (auto& kv : c->mc_graphs) (void)hipGraphExecDestroy(kv.second);  // sa_mc_run's
+  c->mc_graphs.clear();
 }
 
 void free_workspace(sa_ctx* c) {
@@ -453,16 +455,23 @@ int build_tables(sa_ctx* c) {
   std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);  // [G][n][4]; missing sections -> (k 0, +)
   std::vector<uint32_t> fwd2((size_t)((L + 1) / 2) * n, 0);  // [L/2][n] section pairs
   std::vector<uint32_t> fwd3(c->sec3 ? (size_t)c->G3 * n : 0, 0);  // [L/3][n] section triples
-  for (int l = 0; l < L; ++l) {
+  // sections in blocks of 12 over the host's cores (a pair / triple word is
+  // filled by one block); the first bad entry of each section is reported
+  std::vector<std::string> bad((size_t)L);
+  parallel_for(L, 12, [&](int l) {
     const uint32_t* o = c->ordering.data() + (size_t)l * n;
     uint16_t* il = inv.data() + (size_t)l * w;
     for (int r = 0; r < n; ++r) {
       const uint32_t v = o[r];
-      if (v == 0 || v >= (uint32_t)w)
-        return fail(SA_ERR_ORDERING, "ordering[" + std::to_string(l) + "," + std::to_string(r) +
-                                         "] = " + std::to_string(v) + " outside [1, w=" + std::to_string(w) + ")");
-      if (il[v] != (uint16_t)n)
-        return fail(SA_ERR_ORDERING, "ordering row " + std::to_string(l) + " repeats value " + std::to_string(v));
+      if (v == 0 || v >= (uint32_t)w) {
+        bad[l] = "ordering[" + std::to_string(l) + "," + std::to_string(r) + "] = " + std::to_string(v) +
+                 " outside [1, w=" + std::to_string(w) + ")";
+        return;
+      }
+      if (il[v] != (uint16_t)n) {
+        bad[l] = "ordering row " + std::to_string(l) + " repeats value " + std::to_string(v);
+        return;
+      }
       il[v] = (uint16_t)r;
       const uint32_t hi = v >> lgM;
       const uint16_t e = (uint16_t)((v & (uint32_t)(M - 1)) | ((__builtin_popcount(hi) & 1u) << 15));
@@ -471,7 +480,9 @@ int build_tables(sa_ctx* c) {
       if (c->sec3)  // M <= 512: k in 9 bits, the sign in bit 9 of a 10-bit field
         fwd3[(size_t)(l / 3) * n + r] |= (uint32_t)((e & 0x1ffu) | ((e >> 15) << 9)) << (10 * (l % 3));
     }
-  }
+  });
+  for (int l = 0; l < L; ++l)
+    if (!bad[l].empty()) return fail(SA_ERR_ORDERING, bad[l]);
   int rc;
   if ((rc = dev_alloc(c, (void**)&c->d_inv, inv.size() * 2))) return rc;
   if ((rc = dev_alloc(c, (void**)&c->d_fwd, fwd.size() * 2))) return rc;
@@ -486,6 +497,10 @@ int build_tables(sa_ctx* c) {
   if (c->sec3)
     HIP_TRY(hipMemcpyAsync(c->d_fwd3, fwd3.data(), fwd3.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->backend == SA_BACKEND_HADAMARD && c->CB > 0) {  // kept for the batched tables (ensure_invb)
+    c->h_inv = std::move(inv);
+    c->h_fwd = std::move(fwd);
+  }
   return SA_OK;
 }
 
@@ -618,20 +633,18 @@ void banked_section(const sa_ctx* c, int l, const uint16_t* inv_l, uint16_t* out
 // All sections in parallel on the host; uploaded into *dst.
 int build_banked(sa_ctx* c, const std::vector<int>& sets, int gsize, int nbank, uint16_t** dst, int kh) {
   const int L = c->L, n = c->n, w = c->w;
-  std::vector<uint16_t> inv((size_t)L * w, (uint16_t)n), out((size_t)L * w, 0);
+  std::vector<uint16_t> inv_own, out((size_t)L * w, 0);
   std::vector<uint32_t> hs((size_t)L, 0);
-  for (int l = 0; l < L; ++l)
-    for (int r = 0; r < n; ++r) inv[(size_t)l * w + c->ordering[(size_t)l * n + r]] = (uint16_t)r;
-  unsigned nth = std::thread::hardware_concurrency();
-  nth = nth == 0 ? 1 : (nth > 16 ? 16 : nth);
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nth; ++t)
-    th.emplace_back([&, t]() {
-      for (int l = (int)t; l < L; l += (int)nth)
-        banked_section(c, l, inv.data() + (size_t)l * w, out.data() + (size_t)l * w, sets, gsize, nbank,
-                       hs.data(), kh);
+  if (c->h_inv.size() != (size_t)L * w) {  // the host copy went (or never was): rebuild it
+    inv_own.assign((size_t)L * w, (uint16_t)n);
+    parallel_for(L, 1, [&](int l) {
+      for (int r = 0; r < n; ++r) inv_own[(size_t)l * w + c->ordering[(size_t)l * n + r]] = (uint16_t)r;
     });
-  for (auto& x : th) x.join();
+  }
+  const uint16_t* inv = inv_own.empty() ? c->h_inv.data() : inv_own.data();
+  parallel_for(L, 1, [&](int l) {
+    banked_section(c, l, inv + (size_t)l * w, out.data() + (size_t)l * w, sets, gsize, nbank, hs.data(), kh);
+  });
   int rc = dev_alloc(c, (void**)dst, out.size() * 2);
   if (!rc) rc = dev_alloc(c, (void**)&c->d_hs, hs.size() * 4);
   if (rc) return rc;
@@ -776,22 +789,20 @@ int build_fwdb(sa_ctx* c) {
   // same entries build_tables uploads)
   const int lgM = ilog2(c->M);
   const int G = (c->L + kSG - 1) / kSG * (kSG / kSpw);
-  std::vector<uint16_t> fwd((size_t)G * n * kSpw, 0);
-  for (int l = 0; l < c->L; ++l)
-    for (int r = 0; r < n; ++r) {
-      const uint32_t v = c->ordering[(size_t)l * n + r];
-      fwd[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)] =
-          (uint16_t)((v & (uint32_t)(c->M - 1)) | ((__builtin_popcount(v >> lgM) & 1u) << 15));
-    }
-  std::vector<uint16_t> out((size_t)Gb * W * npad, 0);
-  unsigned nth = std::thread::hardware_concurrency();
-  nth = nth == 0 ? 1 : (nth > 16 ? 16 : nth);
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nth; ++t)
-    th.emplace_back([&, t]() {
-      for (int g = (int)t; g < Gb; g += (int)nth) fwdb_group(c, g, fwd.data(), npad, out.data());
+  std::vector<uint16_t> fwd_own;
+  if (c->h_fwd.size() != (size_t)G * n * kSpw) {  // the host copy went (or never was): rebuild it
+    fwd_own.assign((size_t)G * n * kSpw, 0);
+    parallel_for(c->L, 4, [&](int l) {
+      for (int r = 0; r < n; ++r) {
+        const uint32_t v = c->ordering[(size_t)l * n + r];
+        fwd_own[((size_t)(l / kSpw) * n + r) * kSpw + (l % kSpw)] =
+            (uint16_t)((v & (uint32_t)(c->M - 1)) | ((__builtin_popcount(v >> lgM) & 1u) << 15));
+      }
     });
-  for (auto& x : th) x.join();
+  }
+  const uint16_t* fwd = fwd_own.empty() ? c->h_fwd.data() : fwd_own.data();
+  std::vector<uint16_t> out((size_t)Gb * W * npad, 0);
+  parallel_for(Gb, 1, [&](int g) { fwdb_group(c, g, fwd, npad, out.data()); });
   int rc = dev_alloc(c, (void**)&c->d_fwdb, out.size() * 2);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(c->d_fwdb, out.data(), out.size() * 2, hipMemcpyHostToDevice, c->stream));
@@ -834,6 +845,8 @@ int ensure_invb(sa_ctx* c) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
+  std::vector<uint16_t>().swap(c->h_inv);  // the host copies have served
+  std::vector<uint16_t>().swap(c->h_fwd);
   return SA_OK;
 }
 
@@ -848,6 +861,7 @@ int set_lds_limits() {
   hipError_t e = sec_lds_attrs();
   if (e == hipSuccess) e = secb_lds_attrs();
   if (e == hipSuccess) e = dense_lds_attrs();
+  if (e == hipSuccess) e = mc_lds_attrs();
   if (e != hipSuccess) return fail(SA_ERR_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
   done = 1;
   return SA_OK;
@@ -1096,6 +1110,7 @@ void sa_destroy(sa_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   drop_graphs(c);
   free_workspace(c);
+  mc_release(c);
   if (!c->borrowed) {
     dev_free(c->d_inv);
     dev_free(c->d_inv32);

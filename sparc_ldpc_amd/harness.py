@@ -24,7 +24,7 @@ from .operators import SparcOperator, make_ordering, sparc_transforms, sparc_tra
 
 __all__ = [
     "SPARCParams", "LDPCParams", "pa_parameterised", "bits2indices", "ber_of",
-    "amp_ldpc_sim", "mc_decode", "ebno_to_sigma", "ber_point", "waterfall_plain", "amp_test_reps", "amp_init_test",
+    "amp_ldpc_sim", "mc_decode", "mc_decode_batched", "mc_stream", "draw_reps", "ebno_to_sigma", "ber_point", "waterfall_plain", "amp_test_reps", "amp_init_test",
 ]
 
 
@@ -125,7 +125,8 @@ def amp_ldpc_sim(sparcparams: SPARCParams, ldpcparams=None, a=None, f=None, C=No
 def _draw_reps(seeds, L, M, n, sigma):
     """Rep with seed s: ``RandomState(s)`` draws the L section indices uniform
     in [0, M) (the law of random bits -> bits2indices) and then the noise
-    N(0, σ²) (n values) — SURVEY §8d's synthetic inputs."""
+    N(0, σ²) (n values) — SURVEY §8d's synthetic inputs.  (NumPy; draw_reps
+    is the same on the host cores natively.)"""
     idx = np.empty((len(seeds), L), dtype=np.int32)
     noise = np.empty((len(seeds), n))
     for i, s in enumerate(seeds):
@@ -136,16 +137,78 @@ def _draw_reps(seeds, L, M, n, sigma):
     return idx, noise
 
 
-def mc_decode(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True):
-    """Batched Monte-Carlo reps on one device (the rep body of sparc_ldpc.py:
-    423-462 on SURVEY §8d's synthetic inputs, ``_draw_reps``).
+def draw_threads() -> int:
+    """Host threads for draw_reps: the job's CPU share (OMP_NUM_THREADS, 16 on
+    the GPU box), at most the machine's."""
+    want = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(want, os.cpu_count() or 1))
 
-    Encoding x = A β₀ + noise (sa_encode), the decode and the section
-    decisions run on the device; only the indices and the noise cross PCIe.
-    The host draws the next batch while the device decodes the current one
-    (the decode is asynchronous until the decisions are read).  Returns per-rep
-    int64 arrays (bit_errors, iters) in seed order.
-    """
+
+def draw_reps(seeds, L, M, n, sigma, idx=None, noise=None, threads=None):
+    """_draw_reps' reps (RandomState(s).randint(0, M, L), then .randn(n) * σ),
+    bit for bit, drawn by libsparc_amp's native restatement of NumPy's legacy
+    generator over several host threads (sa_draw_reps).  idx / noise: optional
+    (R, L) int32 / (R, n) fp64 arrays (or views) to fill."""
+    from . import _lib
+    lib = _lib.load()
+    seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64) & 0xFFFFFFFF, dtype=np.uint32)
+    R = len(seeds)
+    idx = np.empty((R, L), dtype=np.int32) if idx is None else idx
+    noise = np.empty((R, n)) if noise is None else noise
+    assert idx.shape == (R, L) and idx.dtype == np.int32 and idx.flags.c_contiguous
+    assert noise.shape == (R, n) and noise.dtype == np.float64 and noise.flags.c_contiguous
+    ct = _lib.ct
+    _lib.check(lib.sa_draw_reps(seeds.ctypes.data_as(ct.POINTER(ct.c_uint32)), R, int(L), int(M), int(n),
+                                float(sigma), idx.ctypes.data_as(ct.POINTER(ct.c_int32)),
+                                noise.ctypes.data_as(ct.POINTER(ct.c_double)),
+                                draw_threads() if threads is None else int(threads)))
+    return idx, noise
+
+
+def mc_stream(op: SparcOperator, Pl, T, idx, noise, batch=256, early_stop=True, timings=None):
+    """Decode staged reps (idx (R, L), noise (R, n)) as one stream through
+    ``batch`` slots with per-slot refill (SparcOperator.mc_run): a slot whose
+    exact-τ stop fires takes the next rep at once.  Returns per-rep int64
+    (bit_errors, iters) and the stream's device milliseconds; ``timings``
+    (a dict) receives the host wall seconds of its phases."""
+    import time
+    t0 = time.perf_counter()
+    op.reserve(batch, T)
+    op.stage_power(batch, np.asarray(Pl, dtype=np.float64))
+    t1 = time.perf_counter()
+    op.mc_stage(idx, noise)
+    t2 = time.perf_counter()
+    _, its, errs, ms = op.mc_run(batch, T, early_stop=early_stop, decisions=False)
+    if timings is not None:
+        timings.update(setup_s=t1 - t0, stage_s=t2 - t1, run_s=time.perf_counter() - t2)
+    return errs.astype(np.int64), its.astype(np.int64), ms
+
+
+def mc_decode(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True, stream=None):
+    """Monte-Carlo reps on one device (the rep body of sparc_ldpc.py:423-462
+    on SURVEY §8d's synthetic inputs, ``_draw_reps``).  Returns per-rep int64
+    arrays (bit_errors, iters) in seed order.
+
+    stream (default: wherever the operator supports it, mc_supported): the
+    reps drawn natively on the host cores (draw_reps) and decoded as one
+    stream through ``batch`` refilled slots (mc_stream); else batch by batch
+    (mc_decode_batched).  The per-rep results are the same either way
+    (tests/test_gpu_mc_stream.py)."""
+    seeds = list(seeds)
+    if stream is None:
+        stream = op.mc_supported(batch)
+    if not stream or not seeds:
+        return mc_decode_batched(op, Pl, sigma, T, seeds, batch, early_stop)
+    idx, noise = draw_reps(seeds, op.L, op.M, op.n, sigma)
+    be, it, _ = mc_stream(op, Pl, T, idx, noise, batch, early_stop)
+    return be, it
+
+
+def mc_decode_batched(op: SparcOperator, Pl, sigma, T, seeds, batch=256, early_stop=True):
+    """mc_decode batch by batch: encoding x = A β₀ + noise (sa_encode), the
+    decode and the section decisions on the device, every batch run until its
+    slowest codeword stops; the host draws the next batch while the device
+    decodes the current one."""
     L, M, n = op.L, op.M, op.n
     Pl = np.asarray(Pl, dtype=np.float64)
     seeds = list(seeds)

@@ -72,13 +72,13 @@ def make_ordering(L: int, M: int, n: int, seed: int = 0) -> np.ndarray:
     if hit is not None:
         _ORDER_CACHE.move_to_end(key)
         return hit
-    w = _w_of(n, M)
-    rng = np.random.RandomState(seed)
-    ordering = np.empty((L, n), dtype=np.uint32)
-    idxs = np.arange(1, w, dtype=np.uint32)
-    for ll in range(L):
-        rng.shuffle(idxs)
-        ordering[ll] = idxs[:n]
+    # the same shuffles restated natively (sa_make_ordering: NumPy's legacy
+    # MT19937 and its 1-d shuffle, bit for bit; tests/test_host.py)
+    if not 0 <= int(seed) < 2 ** 32:
+        raise ValueError("Seed must be between 0 and 2**32 - 1")
+    ordering = np.empty((int(L), int(n)), dtype=np.uint32)
+    check(_lib.load().sa_make_ordering(int(L), int(M), int(n), int(seed),
+                                       ordering.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_uint32))))
     ordering.setflags(write=False)
     _ORDER_CACHE[key] = ordering
     while len(_ORDER_CACHE) > 8:
@@ -316,6 +316,43 @@ class SparcOperator:
         return dict(section_kernel=self.SECTION_KERNELS[int(o[0])], partials=int(o[1]), row_splits=int(o[2]),
                     codewords_per_wg=int(o[3]), zz_partials=int(o[4]), w=int(o[5]),
                     row_kernel={1: "k_row2", 2: "k_rowv16B", 3: "k_rowv8B", 4: "k_row2_16", 5: "k_rowc"}.get(int(o[6]), "k_row"), cus=int(o[7]))
+
+    # ---- Monte-Carlo rep stream (sa_mc_stage / sa_mc_run) -------------------
+    def mc_supported(self, B):
+        """Whether sa_mc_run can decode a stream through B slots on this operator
+        (the batched codeword-interleaved Hadamard decode, 4 <= B <= 1024)."""
+        if self.backend != "hadamard" or not 4 <= int(B) <= 1024:
+            return False
+        if 4 * (64 * (8 if self.precision == "fp64" else 4) + 4 * self.L) > 160 * 1024:
+            return False  # the refill kernel's LDS image of the new reps' indices
+        p = self.plan(B)
+        return p["section_kernel"] == "k_secb" and p["row_kernel"] == "k_rowc"
+
+    def mc_stage(self, idx, noise):
+        """Stage reps for mc_run: section indices idx (R, L), noise (R, n) fp64."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        R = idx.shape[0]
+        assert idx.shape == (R, self.L), "idx must be (R, L)"
+        noise = as_f64(noise)
+        assert noise.size == R * self.n, "noise must be (R, n)"
+        check(self._lib.sa_mc_stage(self._ctx, R, idx.ctypes.data_as(_lib.ct.POINTER(_lib.ct.c_int32)), dptr(noise)))
+        self._mc_reps = R
+        return R
+
+    def mc_run(self, B, T, early_stop=True, decisions=True):
+        """Decode the staged reps through B slots with per-slot refill:
+        -> (decisions (R, L) int32 or None, stop indices (R,) int32 (T: ran
+        out), bit errors (R,) int32, device milliseconds of the stream)."""
+        R = int(getattr(self, "_mc_reps", 0))
+        i32 = _lib.ct.POINTER(_lib.ct.c_int32)
+        dec = np.empty((R, self.L), dtype=np.int32) if decisions else None
+        its = np.empty(R, dtype=np.int32)
+        errs = np.empty(R, dtype=np.int32)
+        ms = np.zeros(1)
+        flags = 0 if early_stop else _lib.SA_FLAG_NO_EARLY_STOP
+        check(self._lib.sa_mc_run(self._ctx, int(B), int(T), flags, None if dec is None else dec.ctypes.data_as(i32),
+                                  its.ctypes.data_as(i32), errs.ctypes.data_as(i32), dptr(ms)))
+        return dec, its, errs, float(ms[0])
 
     def plan_batched(self, B):
         """The batched section kernel's work order for B codewords

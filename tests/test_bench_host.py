@@ -124,6 +124,17 @@ def test_n_rank_bench_line_carries_cpu_baseline_and_spread(world):
         assert json.loads(got[r])["value"] == line["value"]
     # value = every rank's codewords over the slowest rank's time
     assert abs(line["value"] - world * pr["value_min"]) <= 1e-3 * line["value"]
+    # the batched legs of the default line: configs[2] in
+    # both precisions and configs[3], each timed over every rank with its own
+    # decisions and roofline
+    legs = line["batched_legs"]
+    assert set(legs) == {"c3", "c3_fp64", "c4"}
+    for tag, leg in legs.items():
+        assert leg["value"] > 0 and leg["ms_per_step"] > 0 and leg["codewords_per_step_per_gpu"] == 256, tag
+        assert leg["decided_steps_rank0"] == leg["steps"] and "frac" in leg["roofline"], tag
+        assert abs(leg["value"] - 256 * leg["steps"] * world / (leg["ms_per_step"] * leg["steps"] / 1e3)) \
+            <= 1e-2 * leg["value"], tag
+    assert legs["c3_fp64"]["dtype"] == "f64" and legs["c4"]["workload"].startswith("BASELINE configs[3]")
 
 
 def test_timed_step_includes_the_decision():

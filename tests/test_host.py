@@ -227,3 +227,40 @@ def test_amp_refuses_operators_of_two_contexts():
         sp.amp(np.zeros(8), 1.0, np.ones(4), 4, 4, 3, AbOp(_Op()), AzOp(_Op()))
     with pytest.raises(ValueError, match="different operators"):
         sp.amp_test(np.zeros(8), 1.0, np.ones(4), 4, 4, 3, AbOp(_Op()), AzOp(_Op()))
+
+
+@pytest.mark.parametrize("L,M,n,sigma", [(768, 512, 7885, 0.6), (16, 100, 33, 1.3), (5, 1, 7, 0.5),
+                                         (64, 16, 256, 0.95), (3, 3, 0, 1.0)])
+def test_native_draws_match_numpy(L, M, n, sigma):
+    """sa_draw_reps (libsparc_amp's host restatement of NumPy's legacy
+    RandomState: MT19937 integer seeding, masked bounded integers, the polar
+    Gaussian) against harness._draw_reps itself — RandomState(s).randint(0, M, L)
+    then .randn(n) * sigma — bit for bit, including a non-power-of-two M (the
+    rejection loop), M = 1 (no draw), n = 0 and the seeds 0 and 2**32 - 1,
+    single- and multi-threaded."""
+    from sparc_ldpc_amd.harness import _draw_reps, draw_reps
+    seeds = list(range(40)) + [2**32 - 1, 123456789]
+    a_idx, a_noise = _draw_reps(seeds, L, M, n, sigma)
+    for th in (1, 3):
+        b_idx, b_noise = draw_reps(seeds, L, M, n, sigma, threads=th)
+        assert np.array_equal(a_idx, b_idx)
+        assert np.array_equal(a_noise, b_noise)
+
+
+@pytest.mark.parametrize("L,M,n,seed", [(768, 512, 8294, 0), (64, 16, 256, 3), (20, 100, 37, 2**32 - 1), (4, 4, 1, 7)])
+def test_native_ordering_matches_numpy(L, M, n, seed):
+    """sa_make_ordering against the reference's own construction
+    (sparc_ldpc.py:107-117: RandomState(seed).shuffle of arange(1, w) per
+    section, cumulatively, the first n kept), restated in NumPy here."""
+    from sparc_ldpc_amd import _lib
+    from sparc_ldpc_amd.operators import _w_of
+    w = _w_of(n, M)
+    rng = np.random.RandomState(seed)
+    ref = np.empty((L, n), dtype=np.uint32)
+    idxs = np.arange(1, w, dtype=np.uint32)
+    for ll in range(L):
+        rng.shuffle(idxs)
+        ref[ll] = idxs[:n]
+    got = np.empty((L, n), dtype=np.uint32)
+    _lib.check(_lib.load().sa_make_ordering(L, M, n, seed, got.ctypes.data_as(ct.POINTER(ct.c_uint32))))
+    assert np.array_equal(got, ref)

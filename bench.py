@@ -269,7 +269,7 @@ def valu_bound(tag, kernel, kernel_ms, cus, clock_ghz=2.4):
             "source": src, "clock_ghz_assumed": clock_ghz}
 
 
-PROFILE_TAGS = {  # (workload, codewords, backend, precision) -> scripts/profile_r04.sh tag
+PROFILE_TAGS = {  # (workload, codewords, backend, precision) -> scripts/profile_set.sh tag
     ("c2", 1, "hadamard", "fp32"): "c2", ("c4", 1, "hadamard", "fp32"): "c4b1",
     ("c3", 256, "hadamard", "fp32"): "c3", ("c4", 256, "hadamard", "fp32"): "c4",
     ("c3", 256, "dense", "fp32"): "c3dense", ("c4", 1, "dense", "fp32"): "dense_l768",

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy the round's profile summaries from gpurun_out/ (scripts/profile_r04.sh)
+"""Copy the round's profile summaries from gpurun_out/ (scripts/profile_set.sh)
 into profiles/<round>_*: kernel stats, PMC traffic per launch (also merged
 into profiles/pmc_traffic.json under the bench's workload key), the
 graph-replayed kernel durations, SQ counters and phase stamps."""

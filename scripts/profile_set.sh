@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-5 profile set (run on the GPU box): per headline workload a rocprofv3
+# The profile set of a round (run on the GPU box): per headline workload a rocprofv3
 # kernel trace with --stats and separate FETCH_SIZE / WRITE_SIZE passes
 # (scripts/profile.sh, which records the sources hash of the build), optional
 # SQ counter passes (scripts/pmc_sq.sh) and the PMC calibration probe.  Raw
-# output under gpurun_out/; scripts/collect_profiles.py r05 copies the
-# summaries to profiles/r05_*.  Stops at the first step that fails.
-#   bash scripts/profile_r04.sh STEP ...
+# output under gpurun_out/; scripts/collect_profiles.py rNN copies the
+# summaries to profiles/rNN_*.  Stops at the first step that fails.
+#   bash scripts/profile_set.sh STEP ...
 #   steps: c2 c2f64 c4b1 c3 c3f64 c4 c4f64 joint dense_l768 c3dense c2matrix c3matrix
 #          sq_c2 sq_c3 sq_c4 sq_c3f64 sq_bp calib
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -42,7 +42,7 @@ for s in "$@"; do
     sq_c4) sq c4 --workload c4 --no-fp64 --steps 1 --warmup 0 ;;
     sq_c3f64) sq c3f64 --workload c3 --precision fp64 --steps 1 --warmup 0 ;;
     sq_bp) SCRIPT=scripts/bp_time.py sq bp 256 ;;
-    calib) bash scripts/calib_r04.sh || exit 1 ;;
+    calib) bash scripts/pmc_calib.sh || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -694,7 +694,7 @@ __device__ __forceinline__ void store_section(real* p, const real (&x)[E], int l
 template <typename real, int E>
 __device__ __forceinline__ real denoise_section(real (&v)[E], const real (&bprev)[E], real* beta_l,
                                                 int lane, int M, real cl, real tau2, real sqrt_n,
-                                                bool store = true) {
+                                                bool store = true, int dead = 0) {
   // u = (beta + Az/sqrt(n)) * sqrt(n Pl) / tau^2 with the two divisions of
   // :213/:215 folded into one per-section scale
   const real inv_sn = (real)1 / sqrt_n;
@@ -706,7 +706,7 @@ __device__ __forceinline__ real denoise_section(real (&v)[E], const real (&bprev
     const int e = elem_index<E>(lane, i);
     const real s = fma(v[i], inv_sn, bprev[i]);   // :213
     const real uu = s * k;                          // :215
-    u[i] = e < M ? uu : neg_inf<real>();
+    u[i] = (e < M && e >= dead) ? uu : neg_inf<real>();  // dead columns of a padded section: beta 0
     mx = u[i] > mx ? u[i] : mx;
   }
   mx = wave_max(mx);                                // :216 (per section)
@@ -909,6 +909,7 @@ struct SecArgs {
   // Monte-Carlo stream (sa_mc_run): per-codeword iteration index t_b (slot_t),
   // -1 for an empty slot; null: every codeword is at iteration t
   const int* tb;
+  int dead;  // leading dead columns of a padded section (sa_ctx::dead; k_sec only)
 };
 
 template <typename real>
@@ -1177,13 +1178,13 @@ constexpr int ilog2c() { return N <= 1 ? 0 : 1 + ilog2c<N / 2>(); }
 // argmax of one section (one wave, lane's elements elem_index<E>), first index
 // on ties as np.argmax (sparc_ldpc.py:452-455); uniform over the wave
 template <typename real, int E>
-__device__ __forceinline__ int section_argmax(const real* bl, int lane, int M) {
+__device__ __forceinline__ int section_argmax(const real* bl, int lane, int M, int dead = 0) {
   real best = neg_inf<real>();
   int bi = 0x7fffffff;
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const int e = elem_index<E>(lane, i);
-    if (e < M) {
+    if (e < M && e >= dead) {
       const real x = bl[e];
       if (x > best || (x == best && e < bi)) { best = x; bi = e; }
     }
@@ -1194,7 +1195,7 @@ __device__ __forceinline__ int section_argmax(const real* bl, int lane, int M) {
     const int oi = __shfl_xor(bi, m);
     if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
   }
-  return bi == 0x7fffffff ? 0 : bi;
+  return bi == 0x7fffffff ? 0 : bi - dead;  // the caller's column (a padded section's dead columns first)
 }
 
 constexpr int kRow2Rows = 32;  // k_row2: one 128-B line of a partial per row block

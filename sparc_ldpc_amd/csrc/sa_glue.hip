@@ -264,6 +264,7 @@ int stage_onehot_impl(sa_ctx* c, int B, const int32_t* idx, double scale, bool a
   if (B <= 0 || B > c->Bcap || !idx) return fail(SA_ERR_ARG, "sa_stage_onehot: bad arguments");
   if (!c->power_set) return fail(SA_ERR_ARG, "sa_stage_onehot: power allocation not staged");
   if (!std::isfinite(scale)) return fail(SA_ERR_ARG, "sa_stage_onehot: scale must be finite");
+  if (c->dead) return fail(SA_ERR_UNSUPPORTED, "sa_stage_onehot: M must be a power of two (bits2indices)");
   for (size_t i = 0; i < (size_t)B * c->L; ++i)
     if (idx[i] >= c->M || (idx[i] < 0 && !(allow_empty && idx[i] == -1)))
       return fail(SA_ERR_ARG, "sa_stage_onehot: index outside [0, M)");

@@ -53,6 +53,10 @@ struct sa_ctx {
   int L = 0, M = 0, n = 0, w = 0, nhi = 0, backend = 0, prec = 0, device = 0;
   int plan = 0;       // SA_PLAN_* options of sa_create_ex (0: every choice by the built-in rules)
   bool pow2 = true;  // M a power of two (the Hadamard kernels, bit-level glue)
+  // the caller's section size Mu; the Hadamard backend pads a section of any
+  // Mu to M = 2^ceil(log2 Mu) columns, the first dead = M - Mu of them never
+  // used (column c of the reference is column dead + c: sparc_ldpc.py:54, 68)
+  int Mu = 0, dead = 0;
   int G = 0, NZ = 0, E = 1;
   int n_cus = 256;
   int Gb = 0, CB = 0;  // batched kernel: groups of WB sections, codewords per workgroup (0 = off)
@@ -266,6 +270,7 @@ SecArgs<real> sec_args(sa_ctx* c, int mode, int t, int early_stop) {
   if (c->pb_on) a.c = (const real*)c->d_cb;
   a.sqrt_n = (real)std::sqrt((double)c->n);
   a.tb = c->mc_tb;
+  a.dead = c->dead;
   return a;
 }
 

@@ -417,11 +417,11 @@ __global__ void __launch_bounds__(NT) k_row2(RowArgs<real> a) {
 
 // Per-section decision (sparc_ldpc.py:452-455): argmax, first index on ties.
 template <typename real, int E>
-__global__ void __launch_bounds__(256) k_decide(const real* beta, int32_t* idx, int L, int M) {
+__global__ void __launch_bounds__(256) k_decide(const real* beta, int32_t* idx, int L, int M, int dead) {
   const int lane = threadIdx.x & 63;
   const int l = blockIdx.x * 4 + (threadIdx.x >> 6), b = blockIdx.y;
   if (l >= L) return;
-  const int bi = section_argmax<real, E>(beta + ((size_t)b * L + l) * M, lane, M);
+  const int bi = section_argmax<real, E>(beta + ((size_t)b * L + l) * M, lane, M, dead);
   if (lane == 0) idx[(size_t)b * L + l] = bi;
 }
 
@@ -471,9 +471,9 @@ int launch_decide(sa_ctx* c, int B) {
 #define SA_DEC(EE)                                                                                             \
   case EE:                                                                                                     \
     if (c->prec == SA_PREC_F64)                                                                                \
-      k_decide<double, EE><<<grid, 256, 0, c->stream>>>((const double*)c->d_beta, c->d_idx, c->L, c->M);      \
+      k_decide<double, EE><<<grid, 256, 0, c->stream>>>((const double*)c->d_beta, c->d_idx, c->L, c->M, c->dead);      \
     else                                                                                                       \
-      k_decide<float, EE><<<grid, 256, 0, c->stream>>>((const float*)c->d_beta, c->d_idx, c->L, c->M);        \
+      k_decide<float, EE><<<grid, 256, 0, c->stream>>>((const float*)c->d_beta, c->d_idx, c->L, c->M, c->dead);        \
     break;
   switch (c->E) { SA_DEC(1) SA_DEC(2) SA_DEC(4) SA_DEC(8) SA_DEC(16) SA_DEC(32) SA_DEC(64) }
 #undef SA_DEC

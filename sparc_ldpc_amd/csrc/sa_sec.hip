@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(256) k_sec(SecArgs<real> a) {
       return;  // uniform: no barrier follows in this mode
     }
     if (have) {
-      const real bb = denoise_section<real, E>(v, bprev, blo, lane, M, cl, tau2, a.sqrt_n, owner);
+      const real bb = denoise_section<real, E>(v, bprev, blo, lane, M, cl, tau2, a.sqrt_n, owner, a.dead);
       if (lane == 0) bbw[wv] = bb;  // per-wave beta^2, summed below in section order
   STAMP(5);
     }
@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(256) k_secg(SecArgs<real> a) {
       return;  // uniform: no barrier follows in this mode
     }
     if (have) {
-      const real bb = denoise_section<real, E>(v, bprev, blo, lane, M, cl, tau2, a.sqrt_n, owner);
+      const real bb = denoise_section<real, E>(v, bprev, blo, lane, M, cl, tau2, a.sqrt_n, owner, a.dead);
       if (lane == 0) bbw[wv] = bb;
     }
   }

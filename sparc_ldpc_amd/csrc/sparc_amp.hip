@@ -359,6 +359,33 @@ int check_op(const sa_ctx* c, const char* what) {
   return SA_OK;
 }
 
+// The caller's section vectors [B][L][Mu] <-> the device's padded layout
+// [B][L][M] (a padded section's dead leading columns zero); identity when M
+// is the caller's.
+int upload_sections(sa_ctx* c, void* dst, const double* src, int B) {
+  const size_t LM = (size_t)c->L * c->M;
+  if (c->dead == 0) return upload(c, dst, src, (size_t)B * LM);
+  std::vector<double> pad((size_t)B * LM, 0.0);
+  for (size_t bl = 0; bl < (size_t)B * c->L; ++bl)
+    std::memcpy(pad.data() + bl * c->M + c->dead, src + bl * c->Mu, (size_t)c->Mu * sizeof(double));
+  int rc = upload(c, dst, pad.data(), pad.size());
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));  // pad is a host temporary
+  return SA_OK;
+}
+
+int download_sections(sa_ctx* c, double* dst, const void* src, int B) {
+  const size_t LM = (size_t)c->L * c->M;
+  if (c->dead == 0) return download(c, dst, src, (size_t)B * LM);
+  std::vector<double> pad((size_t)B * LM);
+  int rc = download(c, pad.data(), src, pad.size());
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (size_t bl = 0; bl < (size_t)B * c->L; ++bl)
+    std::memcpy(dst + bl * c->Mu, pad.data() + bl * c->M + c->dead, (size_t)c->Mu * sizeof(double));
+  return SA_OK;
+}
+
 int set_power(sa_ctx* c, const double* Pl) {
   if (!Pl) return fail(SA_ERR_ARG, "Pl is NULL");
   std::vector<double> cl(c->L);
@@ -883,9 +910,6 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     return fail(SA_ERR_UNSUPPORTED, "dense backend streams an fp32 matrix (precision must be F32)");
   const bool pow2 = (M & (M - 1)) == 0;
   if (M > 4096) return fail(SA_ERR_UNSUPPORTED, "M must be <= 4096");
-  if (!pow2 && backend == SA_BACKEND_HADAMARD)
-    return fail(SA_ERR_UNSUPPORTED, "the matrix-free Hadamard operator needs M a power of two "
-                                    "(the dense and host-operator backends take any M)");
   // the Hadamard operator takes n past 16-bit row indices (k_secg); the
   // materialised designs and the host-operator loop keep the 16-bit limit
   if (n >= (backend == SA_BACKEND_HADAMARD ? (1 << 24) : 65535))
@@ -897,8 +921,20 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
 
   sa_ctx* c = new sa_ctx();
   c->L = L; c->M = M; c->n = n; c->backend = backend; c->prec = prec; c->device = device; c->plan = plan;
+  c->Mu = M;
   const int mx = (M + 1) > (n + 1) ? (M + 1) : (n + 1);
   c->w = 1 << ilog2(mx);  // 2^ceil(log2(max(M+1, n+1))), sparc_ldpc.py:52/:110
+  if (!pow2 && backend == SA_BACKEND_HADAMARD) {
+    // any M on the matrix-free operator: the reference keeps the last M of the
+    // w columns (sparc_ldpc.py:68/:77), which are the last M of the last
+    // Mp = 2^ceil(log2 M) <= w, whose high index bits are all ones: a section
+    // is a padded section of Mp columns whose first Mp - M never carry an
+    // estimate (the denoiser excludes them, beta stays 0 there); the caller's
+    // beta / A^T z move in and out of the padded layout at the boundary
+    c->M = 1 << ilog2(M);
+    c->dead = c->M - M;
+    M = c->M;
+  }
   c->nhi = c->w / M;
   c->E = 1;  // elements per lane of a one-wave section: the power of two covering M
   while (c->E * 64 < M) c->E *= 2;
@@ -920,13 +956,19 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
     c->big = true;
     c->sec_lds = (size_t)kSpw * M * s + (size_t)kSpw * s;
   }
+  if (c->dead > 0 && c->big) {
+    delete c;
+    return fail(SA_ERR_UNSUPPORTED, "M not a power of two: the Hadamard operator keeps z in LDS (n < 65535 and "
+                                    "the z image within 160 KB)");
+  }
   if (c->sec_lds > 160 * 1024) {
     delete c;
     return fail(SA_ERR_UNSUPPORTED, "section kernel does not fit in LDS (n and M too large for this precision)");
   }
   c->G = (L + kSpw - 1) / kSpw;
   c->Gb = (L + kWB - 1) / kWB;  // (re-set after the batched width is chosen)
-  if (M >= 128 && M <= 4096 && !c->big) {  // k_sec2: z + 2 sections' T + top-bit exchange + reductions
+  // (a padded section runs on k_sec alone, the one section kernel that masks dead columns)
+  if (M >= 128 && M <= 4096 && !c->big && c->dead == 0) {  // k_sec2: z + 2 sections' T + top-bit exchange + reductions
     const size_t need = zbytes + 2 * (size_t)M * s + 4 * (size_t)(M / 2) * s + 16 * s;
     if (need <= 160 * 1024) {
       c->G2 = (L + 1) / 2;
@@ -973,8 +1015,9 @@ int create_impl(sa_ctx** out, int L, int M, int n, const uint32_t* ordering, int
       }
       return {0, 0};
     };
-    const auto c8 = c->big ? std::pair<int, size_t>{0, 0} : cb_for(kWB);
-    const auto c16 = c->big ? std::pair<int, size_t>{0, 0} : cb_for(kWB16);
+    const bool nob = c->big || c->dead > 0;
+    const auto c8 = nob ? std::pair<int, size_t>{0, 0} : cb_for(kWB);
+    const auto c16 = nob ? std::pair<int, size_t>{0, 0} : cb_for(kWB16);
     const bool w16 = (plan & SA_PLAN_WB16) ? true
                      : (plan & SA_PLAN_WB8) ? false
                                             : c16.first >= c8.first;
@@ -1087,7 +1130,7 @@ int sa_subset(const sa_ctx* parent, const int64_t* sections, int Ls, sa_ctx** ou
     std::memcpy(ord.data() + (size_t)i * parent->n, parent->ordering.data() + (size_t)s * parent->n,
                 (size_t)parent->n * 4);
   }
-  return create_impl(out, Ls, parent->M, parent->n, ord.data(), parent->backend, parent->prec, parent->device,
+  return create_impl(out, Ls, parent->Mu, parent->n, ord.data(), parent->backend, parent->prec, parent->device,
                      parent->plan);
 }
 
@@ -1100,7 +1143,7 @@ int sa_create_twin(sa_ctx* src, sa_ctx** out) {
   HIP_TRY(hipSetDevice(src->device));
   // the lazily built batched-kernel tables first, so that both contexts use them
   if (int rc = ensure_invb(src)) return rc;
-  return create_impl(out, src->L, src->M, src->n, src->ordering.data(), src->backend, src->prec, src->device,
+  return create_impl(out, src->L, src->Mu, src->n, src->ordering.data(), src->backend, src->prec, src->device,
                      src->plan, src);
 }
 
@@ -1145,8 +1188,7 @@ int sa_Ab(sa_ctx* c, int B, const double* beta, double* out) {
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
   if (rc) return rc;
-  const size_t LM = (size_t)c->L * c->M;
-  if ((rc = upload(c, c->d_beta, beta, (size_t)B * LM))) return rc;
+  if ((rc = upload_sections(c, c->d_beta, beta, B))) return rc;
   rc = c->prec == SA_PREC_F64 ? seq_ab<double>(c, B) : seq_ab<float>(c, B);
   if (rc) return rc;
   if ((rc = download(c, out, c->d_out, (size_t)B * c->n))) return rc;
@@ -1160,7 +1202,6 @@ int sa_Az(sa_ctx* c, int B, const double* z, double* out) {
   HIP_TRY(hipSetDevice(c->device));
   int rc = ensure_workspace(c, B, c->Tcap > 0 ? c->Tcap : 1);
   if (rc) return rc;
-  const size_t LM = (size_t)c->L * c->M;
   if ((rc = upload(c, c->d_z, z, (size_t)B * c->n))) return rc;
   c->zil_last = false;  // d_z holds [B][n] now
   if (c->prec == SA_PREC_F64) {
@@ -1169,7 +1210,7 @@ int sa_Az(sa_ctx* c, int B, const double* z, double* out) {
     rc = seq_az<float>(c, B);
   }
   if (rc) return rc;
-  if ((rc = download(c, out, c->d_out, (size_t)B * LM))) return rc;
+  if ((rc = download_sections(c, out, c->d_out, B))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
 }
@@ -1189,7 +1230,7 @@ int sa_stage(sa_ctx* c, int B, const double* y, const double* Pl, const double* 
   if (rc) return rc;
   if (Pl && (rc = set_power(c, Pl))) return rc;
   if (y && (rc = upload(c, c->d_y, y, (size_t)B * c->n))) return rc;  // NULL: keep the staged y
-  if (beta0 && (rc = upload(c, c->d_beta, beta0, (size_t)B * c->L * c->M))) return rc;
+  if (beta0 && (rc = upload_sections(c, c->d_beta, beta0, B))) return rc;
   return SA_OK;
 }
 
@@ -1256,7 +1297,7 @@ int sa_fetch(sa_ctx* c, int B, double* beta_out, int* iters_out) {
   if (B <= 0 || B > c->Bcap) return fail(SA_ERR_ARG, "sa_fetch: bad batch");
   HIP_TRY(hipSetDevice(c->device));
   int rc;
-  if (beta_out && (rc = download(c, beta_out, c->d_beta, (size_t)B * c->L * c->M))) return rc;
+  if (beta_out && (rc = download_sections(c, beta_out, c->d_beta, B))) return rc;
   if (iters_out) HIP_TRY(hipMemcpyAsync(iters_out, c->d_iters, (size_t)B * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return SA_OK;
@@ -1435,7 +1476,7 @@ int sa_plan_batched(sa_ctx* c, int B, int64_t* o) {
 
 int sa_info(const sa_ctx* c, int64_t* o) {
   if (check_ctx(c) || !o) return fail(SA_ERR_ARG, "sa_info: bad arguments");
-  o[0] = c->L; o[1] = c->M; o[2] = c->n; o[3] = c->w; o[4] = c->backend; o[5] = c->prec;
+  o[0] = c->L; o[1] = c->Mu; o[2] = c->n; o[3] = c->w; o[4] = c->backend; o[5] = c->prec;
   o[6] = c->device; o[7] = (int64_t)c->bytes;
   return SA_OK;
 }

@@ -103,8 +103,9 @@ def test_mfma_c2_batch_golden(sp):
 def test_dense_any_section_size_vs_oracle(sp, L, M, n):
     """M not a power of two (the reference's sub_fht takes any M,
     sparc_ldpc.py:32-79; w = 2^ceil(log2(max(M+1, n+1)))): the dense backend's
-    fp32 GEMVs (B = 1) and int8 GEMMs (B = 6), and the decode, vs the oracle.
-    The matrix-free Hadamard backend refuses such M."""
+    fp32 GEMVs (B = 1) and int8 GEMMs (B = 6), and the decode, vs the oracle;
+    and the same decode on the matrix-free Hadamard backend (padded sections,
+    test_gpu_parity.py::test_hadamard_any_section_size_vs_oracle)."""
     op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="dense")
     oAb, oAz, _ = orc.sparc_transforms(L, M, n)
     rs = np.random.RandomState(M)
@@ -124,5 +125,8 @@ def test_dense_any_section_size_vs_oracle(sp, L, M, n):
             ref = orc._amp_core(ys[b].reshape(-1, 1), Pl, L, M, 8, oAb, oAz, None, early_stop=False)[0]
             assert rel(bb[b], ref) <= 1e-5
             assert np.array_equal(orc.section_argmax(bb[b], L, M), orc.section_argmax(ref, L, M))
-    with pytest.raises(sp.SparcAmpError):
-        sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="hadamard")
+    had = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), backend="hadamard", precision="fp64")
+    hb, _ = had.amp_batch(ys[:6], Pl, 8, early_stop=False)
+    for b in range(6):
+        ref = orc._amp_core(ys[b].reshape(-1, 1), Pl, L, M, 8, oAb, oAz, None, early_stop=False)[0]
+        assert rel(hb[b], ref) <= 1e-11

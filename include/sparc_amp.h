@@ -147,7 +147,9 @@ int sa_amp(sa_ctx* ctx, int B, const double* y, const double* Pl, int T,
 
 /* ---- device-resident path (bench / Monte-Carlo harness) ----------------
  * sa_reserve sizes the device workspace for B codewords and T iterations
- * (it discards staged data when it has to grow); sa_stage copies y (and Pl, and optionally beta0) into the context's device
+ * (it discards staged data when it has to grow) and builds the tables a
+ * decode of B codewords needs that are built lazily (the batched kernel's
+ * bank-aware tables, once per operator); sa_stage copies y (and Pl, and optionally beta0) into the context's device
  * buffers; sa_run decodes the staged batch asynchronously on the context's
  * stream (replayed hipGraph); sa_wait blocks until it is done; sa_fetch
  * copies the results back.  sa_run_event_ms returns the device time of the

@@ -222,7 +222,9 @@ __global__ void __launch_bounds__(256) k_mc_turnover(McArgs a, real* beta) {
 // Every staged rep's channel output and start, before the stream runs (the
 // whole batch of encodes fills the chip; inside the stream's iterations a few
 // refills at a time did not).  Workgroup = one 128-row block of k_rowc x
-// kFillSlots reps, one wave per (rep, 64-row half), a lane per row:
+// kFillSlots reps, one wave per 64-row half, a lane per row carrying the
+// kFillSlots reps' sums side by side (one Ab-table read serves all of them;
+// the reps' section indices are workgroup-uniform scalar loads):
 // y = A beta(idx) + noise with sa_encode's arithmetic (k_colsum: the binary64
 // sum of +-c_l over the sections in order, / sqrt(n), + noise, one rounding to
 // `real`) and the block's z^2 partial exactly as k_rowc's zero start forms it
@@ -232,29 +234,27 @@ __global__ void __launch_bounds__(256) k_mc_turnover(McArgs a, real* beta) {
 constexpr int kFillSlots = 4;
 
 template <typename real>
-__global__ void __launch_bounds__(kFillSlots * 128) k_mc_encode(McArgs a, int nreps, const ushort4* __restrict__ fwd,
-                                                                const double* __restrict__ cd, double sqrt_n,
-                                                                real* __restrict__ y_all, real* __restrict__ zzp_all) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+__global__ void __launch_bounds__(128) k_mc_encode(McArgs a, int nreps, const ushort4* __restrict__ fwd,
+                                                   const double* __restrict__ cd, double sqrt_n,
+                                                   real* __restrict__ y_all, real* __restrict__ zzp_all) {
+  __shared__ real yh[kFillSlots][64];  // the second half's y, for the first half's z^2 partial
   const int j0 = blockIdx.y * kFillSlots;
   const int cnt = nreps - j0 < kFillSlots ? nreps - j0 : kFillSlots;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, n = a.n, L = a.L;
-  const int j = wv >> 1, half = wv & 1;  // this wave's rep of the chunk and half of the block
-  real* yh = reinterpret_cast<real*>(fsm);                                          // [kFillSlots][64] second halves
-  int32_t* sidx = reinterpret_cast<int32_t*>(fsm + kFillSlots * 64 * sizeof(real));  // [kFillSlots][L]
-  for (int i = tid; i < cnt * L; i += kFillSlots * 128)
-    sidx[i] = a.idx[(size_t)(j0 + i / L) * L + i % L];
-  __syncthreads();
-  const bool on = j < cnt;
-  const int rep = j0 + (on ? j : 0);
+  const int lane = threadIdx.x & 63, half = threadIdx.x >> 6, n = a.n, L = a.L;
   const int r = blockIdx.x * 128 + half * 64 + lane;
-  real yv = 0;
-  if (on && r < n) {
-    const int32_t* si = sidx + j * L;
-    double acc = 0.0;
+  // the kFillSlots reps' section indices: uniform over the workgroup (scalar loads)
+  const int32_t* ib = a.idx + (size_t)j0 * L;
+  real yv[kFillSlots];
+#pragma unroll
+  for (int j = 0; j < kFillSlots; ++j) yv[j] = 0;
+  if (r < n) {
+    // kFillSlots independent sums per lane (one per rep), each in section order
+    double acc[kFillSlots];
+#pragma unroll
+    for (int j = 0; j < kFillSlots; ++j) acc[j] = 0.0;
     const int G4 = (L + kSpw - 1) / kSpw;
     // the row's Ab-table entries kFillAhead groups at a time, the next block's
-    // loads in flight while this block's sums run (the sums stay in l order)
+    // loads in flight while this block's sums run
     constexpr int kFillAhead = 16;
     const ushort4* fr = fwd + r;
     ushort4 cur[kFillAhead], nxt[kFillAhead];
@@ -274,29 +274,46 @@ __global__ void __launch_bounds__(kFillSlots * 128) k_mc_encode(McArgs a, int nr
         for (int q = 0; q < 4; ++q) {
           const int l = g * kSpw + q;
           if (l < L) {  // (uniform; no early exit, so that the block stays unrolled)
-            const unsigned kk = fq[q] & 0x7fffu;
-            const unsigned neg = (fq[q] >> 15) ^ (__popc(kk & (unsigned)si[l]) & 1u);
-            acc += neg ? -cd[l] : cd[l];
+            const unsigned kk = fq[q] & 0x7fffu, sg = fq[q] >> 15;
+            const double c = cd[l];
+#pragma unroll
+            for (int j = 0; j < kFillSlots; ++j) {
+              const unsigned id = (unsigned)ib[(size_t)(j < cnt ? j : 0) * L + l];
+              const unsigned neg = sg ^ (__popc(kk & id) & 1u);
+              acc[j] += neg ? -c : c;
+            }
           }
         }
       }
 #pragma unroll
       for (int u = 0; u < kFillAhead; ++u) cur[u] = nxt[u];
     }
-    const double x = acc / sqrt_n;
-    yv = (real)(x + a.noise[(size_t)rep * n + r]);
-    y_all[(size_t)rep * n + r] = yv;
+#pragma unroll
+    for (int j = 0; j < kFillSlots; ++j) {
+      if (j < cnt) {
+        const double x = acc[j] / sqrt_n;
+        yv[j] = (real)(x + a.noise[(size_t)(j0 + j) * n + r]);
+        y_all[(size_t)(j0 + j) * n + r] = yv[j];
+      }
+    }
   }
-  if (half == 1) yh[j * 64 + lane] = yv;
+  if (half == 1) {
+#pragma unroll
+    for (int j = 0; j < kFillSlots; ++j) yh[j][lane] = yv[j];
+  }
   __syncthreads();
-  if (half == 0 && on) {
-    // k_rowc: q = 0; q += z0 z0 (row lane); q += z1 z1 (row 64 + lane), rows past n skipped
-    real q = 0;
-    if (r < n) q += yv * yv;
-    const real y1 = yh[j * 64 + lane];
-    if (r + 64 < n) q += y1 * y1;
-    const real sz = wave_sum(q);
-    if (lane == 0) zzp_all[(size_t)rep * a.NZ + blockIdx.x] = sz;
+  if (half == 0) {
+#pragma unroll
+    for (int j = 0; j < kFillSlots; ++j) {
+      if (j >= cnt) break;
+      // k_rowc: q = 0; q += z0 z0 (row lane); q += z1 z1 (row 64 + lane), rows past n skipped
+      real q = 0;
+      if (r < n) q += yv[j] * yv[j];
+      const real y1 = yh[j][lane];
+      if (r + 64 < n) q += y1 * y1;
+      const real sz = wave_sum(q);
+      if (lane == 0) zzp_all[(size_t)(j0 + j) * a.NZ + blockIdx.x] = sz;
+    }
   }
 }
 
@@ -336,11 +353,6 @@ McArgs mc_args(sa_ctx* c, int B, int T) {
   return a;
 }
 
-template <typename real>
-size_t mc_fill_lds(const sa_ctx* c) {
-  return (size_t)kFillSlots * 64 * sizeof(real) + (size_t)kFillSlots * c->L * sizeof(int32_t);
-}
-
 // the refill of the slots flagged fresh: decisions of the finished, beta = 0,
 // y / z / z^2 partials of the new reps
 template <typename real>
@@ -362,8 +374,7 @@ int mc_turnover(sa_ctx* c, const McArgs& a) {
 // every staged rep's y and z^2 partials (k_mc_encode)
 template <typename real>
 int mc_encode_all(sa_ctx* c, const McArgs& a, int nreps) {
-  k_mc_encode<real><<<dim3(c->NZ2, (nreps + kFillSlots - 1) / kFillSlots), kFillSlots * 128, mc_fill_lds<real>(c),
-                      c->stream>>>(a, nreps, (const ushort4*)c->d_fwd, c->d_cd, std::sqrt((double)c->n),
+  k_mc_encode<real><<<dim3(c->NZ2, (nreps + kFillSlots - 1) / kFillSlots), 128, 0, c->stream>>>(a, nreps, (const ushort4*)c->d_fwd, c->d_cd, std::sqrt((double)c->n),
                                    (real*)c->d_mc_y, (real*)c->d_mc_zzp);
   HIP_TRY(hipGetLastError());
   return SA_OK;
@@ -403,14 +414,8 @@ int mc_ensure_slots(sa_ctx* c, int B) {
 
 }  // namespace
 
-// the fill kernel's dynamic LDS may pass 64 KB (large L)
-hipError_t mc_lds_attrs() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_mc_encode<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     160 * 1024);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)k_mc_encode<double>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  return e;
-}
+// (the stream's kernels use at most 64 KB of LDS: nothing to raise)
+hipError_t mc_lds_attrs() { return hipSuccess; }
 
 void mc_release(sa_ctx* c) {
   for (auto& kv : c->mc_graphs) (void)hipGraphExecDestroy(kv.second);
@@ -521,8 +526,7 @@ int sa_mc_run(sa_ctx* c, int B, int T, int flags, int32_t* dec_out, int32_t* ite
   if (B < 4 || B > kMcStepThreads || T <= 0) return fail(SA_ERR_ARG, "sa_mc_run: B in [4, 1024], T > 0");
   if (c->mc_nreps <= 0) return fail(SA_ERR_ARG, "sa_mc_run: no reps staged (sa_mc_stage)");
   if (!c->shared_power || c->pb_on) return fail(SA_ERR_ARG, "sa_mc_run: one power allocation must be staged");
-  if (c->backend != SA_BACKEND_HADAMARD || !c->pow2 || c->big || !zil_for(c, B) ||
-      (size_t)kFillSlots * (64 * rsz(c) + 4 * (size_t)c->L) > 160 * 1024)
+  if (c->backend != SA_BACKEND_HADAMARD || !c->pow2 || c->big || !zil_for(c, B))
     return fail(SA_ERR_UNSUPPORTED, "sa_mc_run: needs the batched codeword-interleaved Hadamard decode "
                                     "(k_secb + k_rowc)");
   HIP_TRY(hipSetDevice(c->device));

@@ -1219,7 +1219,10 @@ int sa_reserve(sa_ctx* c, int B, int T) {
   if (check_ctx(c)) return SA_ERR_ARG;
   if (B <= 0 || T < 0) return fail(SA_ERR_ARG, "sa_reserve: bad arguments");
   HIP_TRY(hipSetDevice(c->device));
-  return ensure_workspace(c, B, T > 0 ? T : 1);
+  int rc = ensure_workspace(c, B, T > 0 ? T : 1);
+  // the batched kernel's tables (built once per operator) now, not at the first decode
+  if (!rc && c->backend == SA_BACKEND_HADAMARD && use_batched(c, B)) rc = ensure_invb(c);
+  return rc;
 }
 
 int sa_stage(sa_ctx* c, int B, const double* y, const double* Pl, const double* beta0) {

@@ -323,8 +323,6 @@ class SparcOperator:
         (the batched codeword-interleaved Hadamard decode, 4 <= B <= 1024)."""
         if self.backend != "hadamard" or not 4 <= int(B) <= 1024:
             return False
-        if 4 * (64 * (8 if self.precision == "fp64" else 4) + 4 * self.L) > 160 * 1024:
-            return False  # the refill kernel's LDS image of the new reps' indices
         p = self.plan(B)
         return p["section_kernel"] == "k_secb" and p["row_kernel"] == "k_rowc"
 

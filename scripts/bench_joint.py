@@ -139,21 +139,28 @@ def main():
     ap.add_argument("--parts", type=int, default=2,
                     help="concurrent slices of the batch, each on its own streams (joint.JointPipeline); 1: one decoder")
     args = ap.parse_args()
+    print(json.dumps(measure(args)), flush=True)
 
+
+def measure(args, device=None, rank=0, world=1):
+    """One joint measurement (the line main() prints; bench.py's joint leg):
+    every rank decodes its own batch (draws seeded 7000 + rank * B + i), the
+    timed steps bracketed by a barrier and a device wait on each rank, value =
+    all ranks' codewords / the slowest rank's time; the CPU leg on rank 0."""
     import sparc_ldpc_amd as sp
-    from sparc_ldpc_amd import joint
+    from sparc_ldpc_amd import dist, joint
     from sparc_ldpc_amd.harness import ebno_to_sigma
 
     lp = sp.LDPCParams("802.16", "5/6", Z)
     R = 5 / 6
     sigma = ebno_to_sigma(args.ebno, P, R)
-    jd = joint.joint_decoder(L, M, N_SPARC, lp, T, precision=args.precision)
+    jd = joint.joint_decoder(L, M, N_SPARC, lp, T, precision=args.precision, device=device)
     if args.plan:  # A/B of plan options: the same design with sa_create_ex options
         jd.op = sp.SparcOperator(L, M, N_SPARC, sp.make_ordering(L, M, N_SPARC), precision=args.precision,
                                  plan=[p for p in args.plan.split(",") if p])
     B = args.batch
     Pl = P / L * np.ones(L)
-    idx, noise = jd.draw([np.random.RandomState(7000 + i) for i in range(B)], B, sigma)
+    idx, noise = jd.draw([np.random.RandomState(7000 + rank * B + i) for i in range(B)], B, sigma)
     # the whole batch on one decoder: the reference result the pipelined
     # step must reproduce rep for rep
     jd.stage(idx, noise, Pl)
@@ -165,11 +172,14 @@ def main():
     for _ in range(args.warmup):
         r = runner.decode_staged(idx, Pl, "soft", args.soft_iter)
     runner.wait() if args.parts > 1 else jd.op.wait()
+    dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r = runner.decode_staged(idx, Pl, "soft", args.soft_iter)
     runner.wait() if args.parts > 1 else jd.op.wait()
-    elapsed = time.perf_counter() - t0
+    mine = time.perf_counter() - t0
+    dist.barrier()
+    elapsed = float(dist.allreduce_max(np.array([mine]))[0]) if world > 1 else mine
     for k in ("amp", "ldpc", "bp_iters") if ref is not None else ():
         assert np.array_equal(ref[k], r[k]), f"joint decode differs from the one-decoder result ({k})"
     if args.parts > 1:
@@ -214,9 +224,9 @@ def main():
     nmsg = int(code.info()["Nmsg"])
     result = {
         "metric": "joint AMP<->BP decoded codewords/sec (soft exchange, 2 rounds) at L=512,M=512 + 802.16 5/6 LDPC",
-        "value": round(B * args.steps / elapsed, 3),
+        "value": round(B * args.steps * world / elapsed, 3),
         "unit": "codewords/s",
-        "n_gpus": 1,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
@@ -267,11 +277,11 @@ def main():
                    "ldpc_bits_per_round": r["ldpc"].sum(axis=0).tolist(), "bits": int(B * L * 9)},
         "step_share_ms": {k: round(v, 3) for k, v in share.items()},
     }
-    if not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
         result["cpu_baseline"] = cpu_baseline(sigma, args.soft_iter, procs)
         result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
-    print(json.dumps(result), flush=True)
+    return result
 
 
 if __name__ == "__main__":

@@ -36,6 +36,8 @@ print("fp64_leg", d["fp64_leg"]["value"], d["fp64_leg"]["roofline"]["frac"])
 for k, v in d.get("batched_legs", {}).items():
     print(k, v["value"], v["ms_per_step"], v["roofline"]["kernel"], v["roofline"]["frac"])
 print("mc", {k: v for k, v in d.get("mc_stream", {}).items() if k not in ("workload", "note")})
+j = d.get("joint_leg", {})
+print("joint", j.get("value"), j.get("ms_per_step"), j.get("identical_to_one_decoder"), j.get("roofline", {}).get("kernel"), j.get("roofline", {}).get("frac"), j.get("step_share_ms"))
 print("cpu", d["cpu_baseline"]["value"], d["cpu_baseline"]["gpu_over_cpu"])
 PY
 fi

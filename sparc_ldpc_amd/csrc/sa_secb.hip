@@ -593,7 +593,12 @@ __global__ void __launch_bounds__(W * 64, (E <= 8 ? 4 : 1)) k_secb(SecArgs<real>
           V pv;
 #pragma unroll
           for (int c = 0; c < CB; ++c) pv[c] = acc[c];
-          __builtin_nontemporal_store(pv, reinterpret_cast<V*>(a.abp) + ((size_t)chunk * a.G + g) * n + r);
+          // a plain store: the partials stay in the Infinity Cache for k_rowc's
+          // (non-temporal) reads where they fit (C3: 151 MB), where the
+          // non-temporal store sent them to HBM: C3 +3 %, C3 fp64 +1.5 %, C4
+          // +0-2 % (k_rowc 75 -> 71 us), C4 fp64 neutral; plain loads in
+          // k_rowc as well lost (C4 k_rowc 75 -> 101 us)
+          reinterpret_cast<V*>(a.abp)[((size_t)chunk * a.G + g) * n + r] = pv;
         } else {
 #pragma unroll
           for (int c = 0; c < CB; ++c)

@@ -450,6 +450,16 @@ def measure_roofline(op, workload, L, M, n, B, T, precision, ms_per_step):
             "frac_minimal": round(minimal / ((sec_ms + row_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "note": "section + row kernel of one iteration against the tables, z, y and beta bytes it must move "
                     "(the Ab partials written by the section kernel and read by the row kernel excluded)"}
+        if B >= 4:
+            # SURVEY §8(d)'s roofline for the batched case: the dense GEMM
+            # formulation's 4 n L M B flops per iteration (A beta and A^T z),
+            # at the rate the factorised operator delivers them
+            fl = 4.0 * n * L * M * B
+            roof["dense_equivalent"] = {
+                "flops_per_iteration": fl, "tflops": round(fl / ((sec_ms + row_ms) * 1e-3) / 1e12, 1),
+                "over_f32_mfma_peak": round(fl / ((sec_ms + row_ms) * 1e-3) / 1e12 / F32_PEAK_TFLOPS, 2),
+                "note": "the n x (L M) dense products the reference's operator stands for, per second of this "
+                        "iteration, against the fp32 MFMA dense peak (the factorised operator never forms them)"}
     if kname == "k_secb" and precision == "fp32":
         vb = valu_bound(workload, kname, dom_ms, plan["cus"])
         if vb is not None:

@@ -7,7 +7,7 @@
 # summaries to profiles/rNN_*.  Stops at the first step that fails.
 #   bash scripts/profile_set.sh STEP ...
 #   steps: c2 c2f64 c4b1 c3 c3f64 c4 c4f64 joint dense_l768 c3dense c2matrix c3matrix
-#          sq_c2 sq_c3 sq_c4 sq_c3f64 sq_bp calib
+#          sq_c2 sq_c3 sq_c4 sq_c3f64 sq_bp calib mc
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -43,6 +43,12 @@ for s in "$@"; do
     sq_c3f64) sq c3f64 --workload c3 --precision fp64 --steps 1 --warmup 0 ;;
     sq_bp) SCRIPT=scripts/bp_time.py sq bp 256 ;;
     calib) bash scripts/pmc_calib.sh || exit 1 ;;
+    mc)  # the configs[3] rep stream (kernel trace only; the stream's kernels are the batched ones + k_mc_*)
+      rm -rf gpurun_out/prof_mc
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mc -o mc --output-format csv -- \
+        python3 scripts/waterfall.py --sweep l768 --reps 1000 --out /tmp/wf_prof > gpurun_out/prof_mc.txt 2>&1 \
+        || { echo "profile mc failed"; exit 1; }
+      echo "profile mc ok" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

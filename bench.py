@@ -18,7 +18,8 @@ Beside the headline the default line carries the other BASELINE configs,
 each timed on every rank with its own roofline: `fp64_leg` (configs[1] in
 binary64), `batched_legs` (configs[2] C3 B = 256 in binary32 / binary64,
 configs[3] C4 B = 256), `mc_stream` (configs[3]'s 10 k-rep Monte-Carlo sweep,
-one refilled stream) and `joint_leg` (configs[4], the joint AMP<->BP step).
+one refilled stream, with its own CPU baseline) and `joint_leg` (configs[4],
+the joint AMP<->BP step).
 """
 from __future__ import annotations
 
@@ -606,6 +607,22 @@ def mc_stream_leg(sp, args, device, rank, world, make_op=None):
     }
 
 
+def mc_cpu_baseline(leg, procs=None, Tsample=8):
+    """configs[3]'s CPU baseline: the oracle's AMP iterations at L=768 M=512
+    R=5/6 on the host cores (cpu_baseline: `procs` single-threaded processes,
+    Tsample iterations each after a barrier), scaled to the reps the stream
+    decoded: reps/s = iterations/s / (the stream's slot-iterations per rep,
+    the same algorithm's per-rep work, the exact-tau stop included)."""
+    w = dict(WORKLOADS["c4"])
+    per_rep = leg["slot_iterations"] / leg["reps"]
+    base = cpu_baseline(w, procs, Tsample)
+    iters_s = base["value"] * w["T"]  # cpu_baseline scales to T iterations per codeword
+    return {"value": iters_s / per_rep, "unit": "Monte-Carlo reps/s", "cores": base["cores"], "kind": "port",
+            "cpu": base["cpu"], "gpu_over_cpu": round(leg["value"] / (iters_s / per_rep), 1),
+            "sample": f"oracle AMP iterations fp64 NumPy at L=768 M=512 n={n_of(w)}: {base['sample']}; "
+                      f"as reps at the stream's {per_rep:.2f} iterations per rep"}
+
+
 def joint_leg(args, device, rank, world):
     """BASELINE configs[4] (scripts/bench_joint.py's measurement, in this
     process): the joint AMP<->BP soft-exchange step, 256 codewords per GPU as
@@ -799,6 +816,8 @@ def main(argv=None, make_op=None):
         result["cpu_baseline"] = cpu_baseline(w, args.cpu_procs or None, args.cpu_iters or None,
                                               None if ts["last_decisions"] is None else ts["last_decisions"][0])
         result["cpu_baseline"]["gpu_over_cpu"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
+        if "reps" in result.get("mc_stream", {}):
+            result["mc_stream"]["cpu_baseline"] = mc_cpu_baseline(result["mc_stream"], args.cpu_procs or None)
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.finalize()

@@ -31,10 +31,13 @@
 // 32-codeword x 64-row block per plane (NP x 2 MFMA 32x32 tiles, 32 NP int32
 // accumulators per lane), so the planes of one output sit in the same lane
 // and register and recombine with no data movement.  K is streamed in
-// 128-byte stages, double-buffered in LDS (2 x (64 NP + 256) x 128 B) by LDS-DMA
-// (global_load_lds_dwordx4, 1 KB per wave instruction); the 16-byte chunks of
-// every 128-byte LDS row are XOR-swizzled by (row >> 1) & 7 so the operand
-// reads (ds_read_b128, 16 rows per lane group) are bank-conflict free.
+// 128-byte stages by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave
+// instruction): the digit planes (an L2 / Infinity Cache stream, re-read by
+// every row tile) one stage ahead in two buffers, the matrix rows (the HBM
+// stream) two stages ahead in three — 2 x 64 NP x 128 + 3 x 256 x 128 B =
+// 160 KB at NP = 4; the 16-byte chunks of every 128-byte LDS row are
+// XOR-swizzled by (row >> 1) & 7 so the operand reads (ds_read_b128, 16 rows
+// per lane group) are bank-conflict free.
 
 constexpr int kI8TX = 64;               // codewords per workgroup tile
 constexpr int kI8TY = 256;              // matrix rows per workgroup tile
@@ -42,10 +45,12 @@ constexpr int kI8KS = 128;              // K bytes per LDS stage
 constexpr int kI8NPZ = 3, kI8NPB = 4;   // digit planes of z and of beta
 template <int NP> struct I8Tile {
   static constexpr int XR = NP * kI8TX;                // operand (digit-plane) rows per stage
-  static constexpr int Stage = (XR + kI8TY) * kI8KS;   // 57344 / 65536 B
-  static constexpr int Lds = 2 * Stage;                // double buffered
+  static constexpr int XStage = XR * kI8KS;            // 24 / 32 KB
+  static constexpr int YStage = kI8TY * kI8KS;         // 32 KB
+  static constexpr int Lds = 2 * XStage + 3 * YStage;  // X double-, Y triple-buffered: 144 / 160 KB
   static constexpr int DmaX = XR / 8;                  // wave-level DMA instructions per stage: X rows
-  static constexpr int Dma = (XR + kI8TY) / 8;         // ... X + Y rows (56 / 64)
+  static constexpr int DmaY = kI8TY / 8;               // ... Y rows
+  static constexpr int YPerWave = DmaY / 8;            // Y instructions per wave per stage (4)
 };
 constexpr int kI8LdsMax = I8Tile<kI8NPB>::Lds;
 
@@ -65,31 +70,35 @@ struct I8Args {
 
 __device__ __forceinline__ int i8_swz(int r) { return (r >> 1) & 7; }
 
-// One stage (128 K bytes) of the X and Y tiles into LDS: Dma wave
-// instructions, Dma/8 per wave; lane i of an instruction fills LDS row
-// 8q + i/8, 16-B slot i%8, with the global chunk (i%8) ^ swz(row).
+// One stage (128 K bytes) of the X (digit-plane) or Y (matrix) tile into
+// LDS: wave instructions of 1 KB, DmaX / 8 or DmaY / 8 per wave; lane i of an
+// instruction fills LDS row 8q + i/8, 16-B slot i%8, with the global chunk
+// (i%8) ^ swz(row).
 template <int NP>
-__device__ __forceinline__ void i8_stage_load(const I8Args& a, unsigned char* dst, int tx, int ty, long long k0,
-                                              int wv, int lane) {
+__device__ __forceinline__ void i8_load_x(const I8Args& a, unsigned char* dst, int tx, long long k0, int wv, int lane) {
   using Tl = I8Tile<NP>;
   const int slot = lane & 7, rsub = lane >> 3;
 #pragma unroll
-  for (int i = 0; i < Tl::Dma / 8; ++i) {
+  for (int i = 0; i < Tl::DmaX / 8; ++i) {
     const int q = wv + 8 * i;
-    const int8_t* src;
-    unsigned char* d;
-    if (q < Tl::DmaX) {
-      const int rr = 8 * q + rsub;  // X tile row: plane rr / 64, codeword rr % 64
-      const int p = rr / kI8TX, cw = rr % kI8TX;
-      src = a.X + (long long)p * a.xps + (long long)(tx * kI8TX + cw) * a.K + k0 + 16 * (slot ^ i8_swz(rr));
-      d = dst + q * 1024;
-    } else {
-      const int rr = 8 * (q - Tl::DmaX) + rsub;
-      src = a.Y + (long long)(ty * kI8TY + rr) * a.K + k0 + 16 * (slot ^ i8_swz(rr));
-      d = dst + Tl::XR * kI8KS + (q - Tl::DmaX) * 1024;
-    }
+    const int rr = 8 * q + rsub;  // X tile row: plane rr / 64, codeword rr % 64
+    const int p = rr / kI8TX, cw = rr % kI8TX;
+    const int8_t* src = a.X + (long long)p * a.xps + (long long)(tx * kI8TX + cw) * a.K + k0 + 16 * (slot ^ i8_swz(rr));
     __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)d, 16, 0, 0);
+                                     (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
+  }
+}
+template <int NP>
+__device__ __forceinline__ void i8_load_y(const I8Args& a, unsigned char* dst, int ty, long long k0, int wv, int lane) {
+  using Tl = I8Tile<NP>;
+  const int slot = lane & 7, rsub = lane >> 3;
+#pragma unroll
+  for (int i = 0; i < Tl::YPerWave; ++i) {
+    const int q = wv + 8 * i;
+    const int rr = 8 * q + rsub;
+    const int8_t* src = a.Y + (long long)(ty * kI8TY + rr) * a.K + k0 + 16 * (slot ^ i8_swz(rr));
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
   }
 }
 
@@ -128,9 +137,19 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
       scl[g4][i] = a.scale[(long long)(b < a.B ? b : 0) * a.sst];
     }
 
+  // X buffers at 0 and XStage, Y buffers at 2 XStage + {0, 1, 2} YStage
+  unsigned char* const xbuf = smem;
+  unsigned char* const ybuf = smem + 2 * Tl::XStage;
+  static_assert(Tl::YPerWave == 4, "the vmcnt immediates below count 4 Y loads per wave");
   if (st0 < st1) {
-    i8_stage_load<NP>(a, smem, tx, ty, (long long)st0 * kI8KS, wv, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    i8_load_x<NP>(a, xbuf, tx, (long long)st0 * kI8KS, wv, lane);
+    i8_load_y<NP>(a, ybuf, ty, (long long)st0 * kI8KS, wv, lane);
+    if (st0 + 1 < st1) {
+      i8_load_y<NP>(a, ybuf + Tl::YStage, ty, (long long)(st0 + 1) * kI8KS, wv, lane);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // stage st0's loads (Y of st0 + 1 may fly on)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
   }
   const int r31 = lane & 31;
@@ -146,7 +165,7 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int r = wy * 64 + j * 32 + r31;
-    yo[j] = Tl::XR * kI8KS + r * kI8KS;
+    yo[j] = r * kI8KS;
     yz[j] = i8_swz(r);
   }
 #ifdef SA_STAMPS
@@ -157,11 +176,19 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
     g_stamps[13] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+  int yb = 0;  // (st - st0) % 3
   for (int st = st0; st < st1; ++st) {
-    const int buf = (st - st0) & 1;
-    if (st + 1 < st1)
-      i8_stage_load<NP>(a, smem + (buf ^ 1) * Tl::Stage, tx, ty, (long long)(st + 1) * kI8KS, wv, lane);
-    const unsigned char* sb = smem + buf * Tl::Stage;
+    const int xi = (st - st0) & 1;
+    // the buffers stage st - 1 read (freed by the barrier that ended it):
+    // X of st + 1, then Y of st + 2
+    if (st + 1 < st1) i8_load_x<NP>(a, xbuf + (xi ^ 1) * Tl::XStage, tx, (long long)(st + 1) * kI8KS, wv, lane);
+    const bool y2 = st + 2 < st1;
+    if (y2) {
+      const int yn = yb == 0 ? 2 : yb - 1;  // (st + 2) % 3
+      i8_load_y<NP>(a, ybuf + yn * Tl::YStage, ty, (long long)(st + 2) * kI8KS, wv, lane);
+    }
+    const unsigned char* sbx = xbuf + xi * Tl::XStage;
+    const unsigned char* sby = ybuf + yb * Tl::YStage;
     // operand fragments double-buffered across the four 32-deep K steps:
     // step kk + 1's LDS reads issue one between each pair of step kk's MFMAs
     // (sched_group_barrier), so the wait before a step's MFMAs is for reads
@@ -172,9 +199,9 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
       if (kk < kI8KS / 32) {
         const int c = 2 * kk + h;  // this lane's 16-B chunk of the 32-deep K step
 #pragma unroll
-        for (int p = 0; p < NP; ++p) xf[kk & 1][p] = *reinterpret_cast<const i8v4*>(sb + xo[p] + ((c ^ xz[p]) << 4));
+        for (int p = 0; p < NP; ++p) xf[kk & 1][p] = *reinterpret_cast<const i8v4*>(sbx + xo[p] + ((c ^ xz[p]) << 4));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) yf[kk & 1][j] = *reinterpret_cast<const i8v4*>(sb + yo[j] + ((c ^ yz[j]) << 4));
+        for (int j = 0; j < 2; ++j) yf[kk & 1][j] = *reinterpret_cast<const i8v4*>(sby + yo[j] + ((c ^ yz[j]) << 4));
       }
       if (kk > 0) {
         const int q = (kk - 1) & 1;
@@ -196,8 +223,12 @@ __global__ void __launch_bounds__(512) k_gemm_i8(I8Args a) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage's DMA has landed (this wave's)
-    __syncthreads();                                   // ... every wave's, and this stage is consumed
+    // stage st + 1's X and Y have landed (this wave's; Y of st + 2, issued
+    // last, may still fly), then the barrier: every wave's, and stage st is consumed
+    if (y2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    yb = yb == 2 ? 0 : yb + 1;
   }
 
 #ifdef SA_STAMPS

@@ -195,10 +195,10 @@ __global__ void __launch_bounds__(kMcStepThreads) k_mc_step(McArgs a) {
 // took a new rep, the section zeroed (beta = 0, the zero start of
 // sparc_ldpc.py:193-200).
 template <typename real, int E>
-__global__ void __launch_bounds__(256) k_mc_turnover(McArgs a, real* beta) {
+__device__ __forceinline__ void mc_turnover_blocks(const McArgs& a, real* beta, int blk, int nblk) {
   const int lane = threadIdx.x & 63;
   const int nfin = a.ctl[3], G4 = (a.L + 3) / 4;
-  for (int item = blockIdx.x; item < nfin * G4; item += gridDim.x) {
+  for (int item = blk; item < nfin * G4; item += nblk) {
     const int b = a.fin_list[item / G4], l = (item % G4) * 4 + (threadIdx.x >> 6);
     if (l >= a.L) continue;
     const int done = a.done[b];
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) k_mc_turnover(McArgs a, real* beta) {
 // sum of +-c_l over the sections in order, / sqrt(n), + noise, one rounding to
 // `real`) and the block's z^2 partial exactly as k_rowc's zero start forms it
 // (y0 y0 + y1 y1 for rows lane and 64 + lane, then the wave sum).  A refilled
-// slot copies them (k_mc_fill): its state then equals a fresh batched
+// slot copies them (k_mc_turnover's refill blocks): its state then equals a fresh batched
 // decode's after its ROW_INIT0 step.
 constexpr int kFillSlots = 4;
 
@@ -321,12 +321,12 @@ __global__ void __launch_bounds__(128) k_mc_encode(McArgs a, int nreps, const us
 // y, z = y in the codeword-interleaved layout, the partials; grid-stride over
 // the refilled slots' rows.
 template <typename real, int CB>
-__global__ void __launch_bounds__(256) k_mc_fill(McArgs a, const real* __restrict__ y_all,
-                                                 const real* __restrict__ zzp_all, real* __restrict__ y,
-                                                 real* __restrict__ z, real* __restrict__ zzp) {
+__device__ __forceinline__ void mc_fill_blocks(const McArgs& a, const real* __restrict__ y_all,
+                                               const real* __restrict__ zzp_all, real* __restrict__ y,
+                                               real* __restrict__ z, real* __restrict__ zzp, int blk, int nblk) {
   const int nf = a.ctl[4], n = a.n, NZ = a.NZ;
   const long long tot = (long long)nf * n;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < tot; i += (long long)gridDim.x * 256) {
+  for (long long i = blk * 256LL + threadIdx.x; i < tot; i += (long long)nblk * 256) {
     const int slot = a.fresh_list[i / n], r = (int)(i % n);
     const int rep = a.rep[slot];
     const real yv = y_all[(size_t)rep * n + r];
@@ -334,6 +334,16 @@ __global__ void __launch_bounds__(256) k_mc_fill(McArgs a, const real* __restric
     z[((size_t)(slot / CB) * n + r) * CB + (slot % CB)] = yv;
     if (r < NZ) zzp[(size_t)slot * NZ + r] = zzp_all[(size_t)rep * NZ + r];
   }
+}
+
+// The turnover and the refill copy in one launch (independent work behind
+// k_mc_step): blocks [0, gto) run the turnover items, the rest the copy.
+template <typename real, int E, int CB>
+__global__ void __launch_bounds__(256) k_mc_turnover(McArgs a, real* beta, int gto, const real* __restrict__ y_all,
+                                                     const real* __restrict__ zzp_all, real* __restrict__ y,
+                                                     real* __restrict__ z, real* __restrict__ zzp) {
+  if ((int)blockIdx.x < gto) mc_turnover_blocks<real, E>(a, beta, blockIdx.x, gto);
+  else mc_fill_blocks<real, CB>(a, y_all, zzp_all, y, z, zzp, blockIdx.x - gto, gridDim.x - gto);
 }
 
 // ---- host side ------------------------------------------------------------------
@@ -357,16 +367,22 @@ McArgs mc_args(sa_ctx* c, int B, int T) {
 // y / z / z^2 partials of the new reps
 template <typename real>
 int mc_turnover(sa_ctx* c, const McArgs& a) {
-  const int g = std::min(2048, a.B * ((c->L + 3) / 4));
+  const int gto = std::min(2048, a.B * ((c->L + 3) / 4));
+  const int gfill = std::min(4096, (a.B * c->n + 255) / 256);
+  constexpr int CBz = 16 / (int)sizeof(real);
+  const real* ya = (const real*)c->d_mc_y;
+  const real* za = (const real*)c->d_mc_zzp;
   switch (c->E) {
-#define SA_TO(EE) case EE: k_mc_turnover<real, EE><<<g, 256, 0, c->stream>>>(a, (real*)c->d_beta); break;
+#define SA_TO(EE)                                                                                             \
+  case EE:                                                                                                    \
+    k_mc_turnover<real, EE, CBz><<<gto + gfill, 256, 0, c->stream>>>(a, (real*)c->d_beta, gto, ya, za,        \
+                                                                     (real*)c->d_y, (real*)c->d_z,            \
+                                                                     (real*)c->d_zzp);                        \
+    break;
     SA_TO(1) SA_TO(2) SA_TO(4) SA_TO(8) SA_TO(16)
 #undef SA_TO
     default: return fail(SA_ERR_UNSUPPORTED, "sa_mc_run: M > 1024");
   }
-  constexpr int CBz = 16 / (int)sizeof(real);
-  k_mc_fill<real, CBz><<<std::min(4096, (a.B * c->n + 255) / 256), 256, 0, c->stream>>>(
-      a, (const real*)c->d_mc_y, (const real*)c->d_mc_zzp, (real*)c->d_y, (real*)c->d_z, (real*)c->d_zzp);
   HIP_TRY(hipGetLastError());
   return SA_OK;
 }

@@ -135,6 +135,17 @@ def test_n_rank_bench_line_carries_cpu_baseline_and_spread(world):
         assert abs(leg["value"] - 256 * leg["steps"] * world / (leg["ms_per_step"] * leg["steps"] / 1e3)) \
             <= 1e-2 * leg["value"], tag
     assert legs["c3_fp64"]["dtype"] == "f64" and legs["c4"]["workload"].startswith("BASELINE configs[3]")
+    # the whole-iteration figures: minimal bytes = section + row bytes less the
+    # Ab-partial hand-off; the dense GEMM formulation's 4 n L M B flops
+    import bench
+    for tag, wl in (("c3", "c3"), ("c4", "c4")):
+        r = legs[tag]["roofline"]
+        w = bench.WORKLOADS[wl]
+        n, L, M = bench.n_of(w), w["L"], w["M"]
+        it, de = r["iteration"], r["dense_equivalent"]
+        assert it["minimal_bytes"] > 0 and it["partials_bytes"] > 0 and 0 < it["frac_minimal"] < r["frac"] + 1, tag
+        assert de["flops_per_iteration"] == 4.0 * n * L * M * 256, tag
+        assert abs(de["tflops"] - de["flops_per_iteration"] / (it["ms"] * 1e-3) / 1e12) <= 0.1 + 1e-3 * de["tflops"], tag
 
 
 def test_timed_step_includes_the_decision():

@@ -260,27 +260,38 @@ __global__ void __launch_bounds__(128) k_mc_encode(McArgs a, int nreps, const us
     ushort4 cur[kFillAhead], nxt[kFillAhead];
 #pragma unroll
     for (int u = 0; u < kFillAhead; ++u) cur[u] = fr[(size_t)(u < G4 ? u : 0) * n];
+    // per rep, its row of section indices (uniform: scalar loads at constant
+    // offsets from a base advanced once per block)
+    const int32_t* rows[kFillSlots];
+#pragma unroll
+    for (int j = 0; j < kFillSlots; ++j) rows[j] = ib + (size_t)(j < cnt ? j : 0) * L;
     for (int g0 = 0; g0 < G4; g0 += kFillAhead) {
 #pragma unroll
       for (int u = 0; u < kFillAhead; ++u) {
         const int gn = g0 + kFillAhead + u;
         nxt[u] = fr[(size_t)(gn < G4 ? gn : 0) * n];
       }
+      const double* cb = cd + (size_t)g0 * kSpw;
+      const int32_t* rb[kFillSlots];
+#pragma unroll
+      for (int j = 0; j < kFillSlots; ++j) rb[j] = rows[j] + (size_t)g0 * kSpw;
 #pragma unroll
       for (int u = 0; u < kFillAhead; ++u) {
-        const int g = g0 + u;
         const unsigned short fq[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int l = g * kSpw + q;
-          if (l < L) {  // (uniform; no early exit, so that the block stays unrolled)
-            const unsigned kk = fq[q] & 0x7fffu, sg = fq[q] >> 15;
-            const double c = cd[l];
+          const int o = u * kSpw + q;
+          if ((g0 * kSpw) + o < L) {  // (uniform; no early exit, so that the block stays unrolled)
+            const unsigned kk = fq[q] & 0x7fffu;
+            // +-c_l as its bits: the row's sign (sg) folded into the high word once,
+            // each rep's parity bit xored into it (exactly -c or c, as a select would give)
+            const unsigned long long cbits = (unsigned long long)__double_as_longlong(cb[o]);
+            const unsigned chi = (unsigned)(cbits >> 32) ^ ((unsigned)(fq[q] >> 15) << 31);
+            const unsigned clo = (unsigned)cbits;
 #pragma unroll
             for (int j = 0; j < kFillSlots; ++j) {
-              const unsigned id = (unsigned)ib[(size_t)(j < cnt ? j : 0) * L + l];
-              const unsigned neg = sg ^ (__popc(kk & id) & 1u);
-              acc[j] += neg ? -c : c;
+              const unsigned par = (unsigned)__popc(kk & (unsigned)rb[j][o]) << 31;
+              acc[j] += __longlong_as_double((long long)(((unsigned long long)(chi ^ par) << 32) | clo));
             }
           }
         }

@@ -1079,3 +1079,43 @@ def test_batch256_fp32_every_element_vs_f64_oracle(sp, fixture, passes):
             assert per_sec.max() <= 1e-5, (T, s, per_sec.max())
             assert per_el <= 1e-5, (T, s, per_el)
         assert np.array_equal(b[0], b[B - 1])
+
+
+@pytest.mark.parametrize("fixture", ["c2.npz", "c4.npz"])
+def test_batch256_fp64_every_element_vs_oracle(sp, fixture):
+    """The binary64 batched path (k_secb<double> + k_rowc<double>, CB = 2: 128
+    codeword chunks) at B = 256, the launch shape of the fp64 legs and of the
+    joint step's AMP, pinned element by element on every section: slots 0,
+    129 and 255 (first, a middle and the last chunk) hold the fixture's
+    codeword 0, the rest permuted copies, decoded T = 1 and 16 iterations
+    without the stop against the binary64 oracle on the same y.  Bars:
+    TOL["fp64"] on the whole vector and 1e-11 of the section scale on every
+    section's error norm and every element; the three slots bit-identical
+    (a codeword's decode does not depend on its slot)."""
+    g = golden(fixture)
+    L, M, n = (int(g[k]) for k in ("L", "M", "n"))
+    B = 256
+    op = sp.SparcOperator(L, M, n, sp.make_ordering(L, M, n), precision="fp64")
+    assert op.plan(B)["section_kernel"] == "k_secb"
+    Pl = float(g["P"]) / L * np.ones(L)
+    c = np.sqrt(n * Pl[0])
+    oAb, oAz, _ = orc.sparc_transforms(L, M, n)
+    y0 = (g["y_0"] if "y_0" in g else g["y"]).reshape(-1)
+    slots = (0, 129, B - 1)
+    Y = np.empty((B, n))
+    for s in range(B):
+        rs = np.random.RandomState(9000 + s)
+        Y[s] = y0 if s in slots else y0[rs.permutation(n)]
+    for T in (1, 16):
+        b, _ = op.amp_batch(Y, Pl, T, early_stop=False)
+        ref = orc.amp(y0.reshape(-1, 1), 0, Pl, L, M, T, oAb, oAz).reshape(-1)
+        for s in slots:
+            d = (b[s] - ref).reshape(L, M)
+            assert rel(b[s], ref) <= TOL["fp64"], (T, s, rel(b[s], ref))
+            per_sec = np.linalg.norm(d, axis=1) / c
+            per_el = np.abs(d).max() / c
+            print(f"T={T} slot {s}: norm-rel {rel(b[s], ref):.3e}, worst section {per_sec.max():.3e}, "
+                  f"worst element {per_el:.3e}")
+            assert per_sec.max() <= 1e-11, (T, s, per_sec.max())
+            assert per_el <= 1e-11, (T, s, per_el)
+        assert np.array_equal(b[0], b[129]) and np.array_equal(b[0], b[B - 1])
